@@ -1,0 +1,335 @@
+// f2a_host.hip -- host-side helpers shared by the C-ABI files: error reporting, handle
+// validation, transfers, and the derived mesh plans (node->edge CSR in ascending edge order,
+// node clusters) that the gather kernels run on.
+#include "f2a_host.hpp"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace f2a {
+
+namespace {
+std::mutex g_mutex;
+int g_path = -1;
+thread_local std::string g_last_error;
+}  // namespace
+
+int g_resident = 0;
+
+void report(const char *fmt, ...)
+{
+    char msg[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    g_last_error = msg;
+    fprintf(stderr, "fesom2-accelerate: %s\n", msg);
+}
+
+bool ok(hipError_t st, const char *what)
+{
+    if (st == hipSuccess) return true;
+    report("HIP error \"%s\" in %s: %s", hipGetErrorName(st), what, hipGetErrorString(st));
+    return false;
+}
+
+const char *last_error() { return g_last_error.c_str(); }
+
+int kernel_path()
+{
+    if (g_path < 0) {
+        const char *p = getenv("FESOM2_PATH");
+        g_path = (p && (!strcmp(p, "stepwise") || !strcmp(p, "1"))) ? 1 : 0;
+    }
+    return g_path;
+}
+
+void set_kernel_path(int p) { g_path = p == 1 ? 1 : 0; }
+
+int num_kernels_limit()
+{
+    const char *p = getenv("FESOM2_NUM_KERNELS");  // reference NUM_KERNELS, src/fesom2-accelerate.cu:256
+    return p ? atoi(p) : 10;
+}
+
+Buffer *buf(void **h, const char *name)
+{
+    if (!h || !*h) {
+        report("null handle for %s", name);
+        return nullptr;
+    }
+    Buffer *b = static_cast<Buffer *>(*h);
+    if (b->magic != Buffer::kMagic) {
+        report("invalid handle for %s (not created by this library)", name);
+        return nullptr;
+    }
+    return b;
+}
+
+Buffer *need(void **h, size_t bytes, const char *name)
+{
+    Buffer *b = buf(h, name);
+    if (b && b->size < bytes) {
+        report("%s holds %zu bytes, the call needs %zu", name, b->size, bytes);
+        return nullptr;
+    }
+    return b;
+}
+
+hipStream_t stream_of(void **s)
+{
+    if (!s || !*s) return nullptr;
+    return *static_cast<hipStream_t *>(*s);
+}
+
+Buffer *allocate(void *host, size_t bytes, bool create_event)
+{
+    auto *m = new Buffer;
+    m->host_pointer = host;
+    m->size = bytes;
+    if (!ok(hipMalloc(&m->device_pointer, bytes ? bytes : 8), "hipMalloc")) {
+        delete m;
+        return nullptr;
+    }
+    if (create_event) {
+        if (!ok(hipEventCreateWithFlags(&m->event, hipEventDisableTiming), "hipEventCreate")) {
+            (void)hipFree(m->device_pointer);
+            delete m;
+            return nullptr;
+        }
+        m->has_event = true;
+    }
+    return m;
+}
+
+bool h2d(Buffer *b, bool sync, hipStream_t s, bool record)
+{
+    if (!b->host_pointer || !b->size) return true;
+    if (sync) return ok(hipMemcpy(b->device_pointer, b->host_pointer, b->size, hipMemcpyHostToDevice), "H2D");
+    if (!ok(hipMemcpyAsync(b->device_pointer, b->host_pointer, b->size, hipMemcpyHostToDevice, s), "H2D async"))
+        return false;
+    if (record && b->has_event) return ok(hipEventRecord(b->event, s), "hipEventRecord");
+    return true;
+}
+
+bool d2h_async(Buffer *b, hipStream_t s)
+{
+    if (!b->host_pointer || !b->size) return true;
+    return ok(hipMemcpyAsync(b->host_pointer, b->device_pointer, b->size, hipMemcpyDeviceToHost, s), "D2H async");
+}
+
+void wait_event(Buffer *b, hipStream_t s)
+{
+    if (b->has_event) (void)hipStreamWaitEvent(s, b->event, 0);
+}
+
+bool check_levels(int nl, const char *who)
+{
+    if (nl < 2) {
+        report("%s: nl = %d (needs >= 2)", who, nl);
+        return false;
+    }
+    return true;
+}
+
+DeviceArrays::~DeviceArrays()
+{
+    for (void *p : ptrs) (void)hipFree(p);
+}
+
+void *DeviceArrays::alloc(size_t bytes)
+{
+    void *p = nullptr;
+    if (!ok(hipMalloc(&p, std::max<size_t>(bytes, 8)), "hipMalloc(plan)")) return nullptr;
+    ptrs.push_back(p);
+    return p;
+}
+
+// ----------------------------------------------------------------------------- plans
+
+std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
+                                 int n_csr, int nl, std::string &err)
+{
+    auto plan = std::make_unique<Plan>();
+    MeshPlanDev &d = plan->dev;
+    d.n_owned = n_owned;
+    d.n_total = n_total;
+    d.n_edges = n_edges;
+    d.nl = nl;
+    const int L = nl - 1;
+    char msg[256];
+    auto fail = [&](const char *s) {
+        err = s;
+        return std::unique_ptr<Plan>();
+    };
+    // ---- node -> edge CSR.  Filling it in ascending edge order reproduces the order in which the
+    // reference's edge loops add into each node (reference.cpp:406-425).
+    std::vector<int> lev(n_edges);
+    std::vector<int> ptr((size_t)n_csr + 1, 0);
+    for (int e = 0; e < n_edges; e++) {
+        const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
+        const int el1 = m.edge_tri[2 * (size_t)e] - 1, el2 = m.edge_tri[2 * (size_t)e + 1] - 1;
+        if (n1 < 0 || n1 >= n_total || n2 < 0 || n2 >= n_total) {
+            snprintf(msg, sizeof msg, "edges(:,%d) = (%d,%d) outside 1..%d", e + 1, n1 + 1, n2 + 1, n_total);
+            return fail(msg);
+        }
+        if (el1 < 0 || el1 >= m.n_elem_total || el2 < -1 || el2 >= m.n_elem_total) {
+            snprintf(msg, sizeof msg, "edge_tri(:,%d) = (%d,%d) outside 1..%ld", e + 1, el1 + 1, el2 + 1,
+                     m.n_elem_total);
+            return fail(msg);
+        }
+        const int nl1 = m.nlev_elem[el1] - 1, nl2 = el2 >= 0 ? m.nlev_elem[el2] - 1 : 0;  // reference.cpp:412-414
+        lev[e] = std::max(nl1, nl2);
+        if (lev[e] > L || lev[e] < 0) {
+            snprintf(msg, sizeof msg, "edge %d carries %d levels, nl-1 = %d", e + 1, lev[e], L);
+            return fail(msg);
+        }
+        plan->lmax_edges = std::max(plan->lmax_edges, lev[e]);
+        if (n1 < n_csr) ptr[n1 + 1]++;
+        if (n2 < n_csr) ptr[n2 + 1]++;
+    }
+    for (int n = 0; n < n_csr; n++) ptr[n + 1] += ptr[n];
+    std::vector<EdgeRef> refs(ptr[n_csr]);
+    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+    for (int e = 0; e < n_edges; e++) {
+        const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
+        if (n1 < n_csr) refs[pos[n1]++] = {e, n2, lev[e], 0};
+        if (n2 < n_csr) refs[pos[n2]++] = {e, n1, lev[e], 1};
+    }
+    d.edge_ptr = plan->mem.upload(ptr);
+    d.edges = plan->mem.upload(refs);
+    if (!d.edge_ptr || !d.edges) return fail("device allocation for the edge plan failed");
+    // ---- clusters: the nodes of the elements around each owned node (reference.cpp:358-378
+    // takes the bound over those elements' UV_rhs, which a2 built from their 3 nodes).
+    if (m.elem_nodes && m.nie && m.nie_num) {
+        std::vector<int> rptr((size_t)n_owned + 1, 0), zdry(n_owned);
+        std::vector<RingRef> ring;
+        ring.reserve((size_t)n_owned * 7);
+        for (int n = 0; n < n_owned; n++) {
+            const int ne = m.nie_num[n];
+            if (ne < 1 || ne > m.dim) {
+                snprintf(msg, sizeof msg, "nod_in_elem2D_num(%d) = %d outside 1..%d", n + 1, ne, m.dim);
+                return fail(msg);
+            }
+            int zd = 1 << 30;
+            const size_t start = ring.size();
+            for (int k = 0; k < ne; k++) {
+                const int e = m.nie[(size_t)n * m.dim + k] - 1;
+                if (e < 0 || e >= m.n_elem_total) {
+                    snprintf(msg, sizeof msg, "nod_in_elem2D(%d,%d) = %d outside 1..%ld", k + 1, n + 1, e + 1,
+                             m.n_elem_total);
+                    return fail(msg);
+                }
+                const int le = m.nlev_elem[e] - 1;
+                zd = std::min(zd, le);
+                for (int j = 0; j < 3; j++) {
+                    const int v = m.elem_nodes[3 * (size_t)e + j] - 1;
+                    if (v < 0 || v >= n_total) {
+                        snprintf(msg, sizeof msg, "elem2D_nodes(%d,%d) = %d outside 1..%d", j + 1, e + 1, v + 1, n_total);
+                        return fail(msg);
+                    }
+                    size_t q = start;
+                    while (q < ring.size() && ring[q].node != v) q++;
+                    if (q == ring.size())
+                        ring.push_back({v, le});
+                    else
+                        ring[q].lev = std::max(ring[q].lev, le);
+                }
+            }
+            zdry[n] = zd;
+            rptr[n + 1] = (int)ring.size();
+        }
+        d.ring_ptr = plan->mem.upload(rptr);
+        d.ring = plan->mem.upload(ring);
+        d.zdry = plan->mem.upload(zdry);
+        if (!d.ring_ptr || !d.ring || !d.zdry) return fail("device allocation for the cluster plan failed");
+        plan->has_ring = true;
+    }
+    return plan;
+}
+
+namespace {
+using PlanKey = std::tuple<const void *, const void *, const void *, const void *, const void *,
+                           const void *, int, int, int, int, int>;
+std::map<PlanKey, std::unique_ptr<Plan>> g_plans;
+
+template <class T>
+std::vector<T> fetch(Buffer *b, size_t count)
+{
+    std::vector<T> v(count);
+    if (count) (void)hipMemcpy(v.data(), b->device_pointer, count * sizeof(T), hipMemcpyDeviceToHost);
+    return v;
+}
+}  // namespace
+
+const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
+                     bool with_ring)
+{
+    std::lock_guard<std::mutex> lock(g_mutex);
+    PlanKey key{h.edges, h.edge_tri, h.nlev_elem, with_ring ? h.elem_nodes : nullptr,
+                with_ring ? h.nie : nullptr, with_ring ? h.nie_num : nullptr,
+                n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0};
+    auto it = g_plans.find(key);
+    if (it != g_plans.end()) return it->second.get();
+    if (h.edges->size < 2 * sizeof(int) * (size_t)n_edges || h.edge_tri->size < 2 * sizeof(int) * (size_t)n_edges) {
+        report("edge handles hold fewer than myDim_edge2D = %d edges", n_edges);
+        return nullptr;
+    }
+    HostMesh m;
+    std::vector<int> edges = fetch<int>(h.edges, 2 * (size_t)n_edges);
+    std::vector<int> etri = fetch<int>(h.edge_tri, 2 * (size_t)n_edges);
+    m.n_elem_total = (long)(h.nlev_elem->size / sizeof(int));
+    std::vector<int> nle = fetch<int>(h.nlev_elem, m.n_elem_total);
+    m.edges = edges.data();
+    m.edge_tri = etri.data();
+    m.nlev_elem = nle.data();
+    std::vector<int> en, nie, nnum;
+    if (with_ring) {
+        if (h.elem_nodes->size < 3 * sizeof(int) * (size_t)m.n_elem_total) {
+            report("elem2D_nodes holds fewer than 3 x %ld entries", m.n_elem_total);
+            return nullptr;
+        }
+        if (h.nie->size < sizeof(int) * (size_t)h.dim * n_owned || h.nie_num->size < sizeof(int) * (size_t)n_owned) {
+            report("nod_in_elem2D handles hold fewer than myDim_nod2D = %d columns", n_owned);
+            return nullptr;
+        }
+        en = fetch<int>(h.elem_nodes, 3 * (size_t)m.n_elem_total);
+        nie = fetch<int>(h.nie, (size_t)h.dim * n_owned);
+        nnum = fetch<int>(h.nie_num, n_owned);
+        m.elem_nodes = en.data();
+        m.nie = nie.data();
+        m.nie_num = nnum.data();
+        m.dim = h.dim;
+    }
+    std::string err;
+    auto plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, err);
+    if (!plan) {
+        report("invalid mesh: %s", err.c_str());
+        return nullptr;
+    }
+    const Plan *p = plan.get();
+    g_plans[key] = std::move(plan);
+    return p;
+}
+
+void drop_plans_of(const Buffer *b)
+{
+    std::lock_guard<std::mutex> lock(g_mutex);
+    for (auto it = g_plans.begin(); it != g_plans.end();) {
+        const PlanKey &k = it->first;
+        if (std::get<0>(k) == b || std::get<1>(k) == b || std::get<2>(k) == b || std::get<3>(k) == b ||
+            std::get<4>(k) == b || std::get<5>(k) == b)
+            it = g_plans.erase(it);
+        else
+            ++it;
+    }
+}
+
+}  // namespace f2a

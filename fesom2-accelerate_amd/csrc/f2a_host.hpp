@@ -1,0 +1,85 @@
+// f2a_host.hpp -- host-side helpers shared by the C-ABI translation units.
+#pragma once
+#include "f2a_internal.hpp"
+#include "../../include/fesom2-accelerate.h"
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace f2a {
+
+// ---- error reporting (stderr + thread-local last error, like the reference's errorHandling,
+//      include/fesom2-accelerate.h:38-46)
+void report(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+bool ok(hipError_t st, const char *what);
+const char *last_error();
+
+// ---- global modes
+extern int g_resident;  // fesom2_set_resident_
+int kernel_path();      // 0 fused, 1 stepwise
+void set_kernel_path(int p);
+int num_kernels_limit();
+
+// ---- handles
+Buffer *buf(void **h, const char *name);
+Buffer *need(void **h, size_t bytes, const char *name);
+hipStream_t stream_of(void **s);
+Buffer *allocate(void *host, size_t bytes, bool create_event);
+bool h2d(Buffer *b, bool sync, hipStream_t s, bool record);
+bool d2h_async(Buffer *b, hipStream_t s);
+void wait_event(Buffer *b, hipStream_t s);
+template <class T>
+inline T *dptr(Buffer *b)
+{
+    return static_cast<T *>(b->device_pointer);
+}
+inline size_t col_bytes(long cols, int stride) { return (size_t)cols * stride * sizeof(real); }
+bool check_levels(int nl, const char *who);
+
+// ---- device allocations owned by a plan (freed with it)
+struct DeviceArrays {
+    std::vector<void *> ptrs;
+    ~DeviceArrays();
+    void *alloc(size_t bytes);
+    template <class T>
+    T *upload(const std::vector<T> &v)
+    {
+        T *p = static_cast<T *>(alloc(v.size() * sizeof(T)));
+        if (p && !v.empty() && !ok(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "H2D(plan)"))
+            return nullptr;
+        return p;
+    }
+};
+
+// ---- derived mesh structures
+struct HostMesh {  // host views of the connectivity a plan is built from (nullptr = absent)
+    const int *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr;
+    const int *elem_nodes = nullptr, *nie = nullptr, *nie_num = nullptr;
+    long n_elem_total = 0;
+    int dim = 0;
+};
+
+struct Plan {
+    MeshPlanDev dev;
+    DeviceArrays mem;
+    bool has_ring = false;
+    int lmax_edges = 0;
+};
+
+// Node->edge CSR for nodes [0, n_csr) in ascending edge order; clusters for [0, n_owned) when the
+// element connectivity is present.  Validates every index; returns nullptr with `err` set.
+std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
+                                 int n_csr, int nl, std::string &err);
+
+struct MeshHandles {
+    Buffer *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr;
+    Buffer *elem_nodes = nullptr, *nie = nullptr, *nie_num = nullptr;
+    int dim = 0;
+};
+// Cached per (handles, partition sizes); built synchronously on first use.
+const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
+                     bool with_ring);
+void drop_plans_of(const Buffer *b);
+
+}  // namespace f2a

@@ -1,0 +1,117 @@
+// f2a_internal.hpp -- internal types shared by the host orchestration and the HIP kernels.
+//
+// Not part of the public C-ABI (that is include/fesom2-accelerate.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace f2a {
+
+using real = double;
+
+// Buffer handle returned through void** (replaces the reference's struct gpuMemory,
+// include/fesom2-accelerate.h:19-28).  `magic` lets every entry point reject a stale or foreign
+// handle loudly instead of dereferencing it.
+struct Buffer {
+    static constexpr uint32_t kMagic = 0xF2A0B0F1u;
+    uint32_t magic = kMagic;
+    void *host_pointer = nullptr;
+    void *device_pointer = nullptr;
+    size_t size = 0;  // bytes
+    hipEvent_t event = nullptr;
+    bool has_event = false;
+};
+
+// One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the
+// order in which the reference's edge loops touch the node: reference.cpp:406-425).
+struct EdgeRef {
+    int edge;   // 0-based local edge
+    int other;  // 0-based other endpoint
+    int lev;    // max(nl1, nl2) = levels the edge carries (reference.cpp:412-414)
+    int flags;  // bit0: this node is edges(2,e) (second endpoint); bit1: this node writes fct_adf_h(:,e)
+};
+
+// One node of a node's cluster (the union of the nodes of its adjacent elements).  `lev` is the
+// number of levels on which the node takes part in the cluster bound:
+// max over adjacent elements e that contain it of (nlevels(e) - 1)  (reference.cpp:331, :363-377).
+struct RingRef {
+    int node;
+    int lev;
+};
+
+// Device-side view of the derived mesh structures of one (mesh, partition) pair.
+struct MeshPlanDev {
+    int n_owned = 0;       // myDim_nod2D
+    int n_total = 0;       // myDim_nod2D + eDim_nod2D
+    int n_edges = 0;       // myDim_edge2D
+    int nl = 0;
+    // node -> incident edges, owned nodes only
+    const int *edge_ptr = nullptr;     // [n_owned + 1]
+    const EdgeRef *edges = nullptr;    // [edge_ptr[n_owned]]
+    // node -> cluster nodes, owned nodes only (needs elem2D_nodes / nod_in_elem2D)
+    const int *ring_ptr = nullptr;     // [n_owned + 1]
+    const RingRef *ring = nullptr;
+    const int *zdry = nullptr;         // [n_owned] min over adjacent elements of (nlevels(e)-1)
+    // local edges with no owned endpoint (b3-horizontal still applies to them)
+    const int *orphan_edges = nullptr;
+    int n_orphans = 0;
+};
+
+// Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().
+struct P1Args {
+    int n_owned, nl, vlimit;
+    const int *nlev_nod;
+    const real *ttf, *LO, *adf_v, *adf_h, *area_inv;
+    real *plus, *minus;
+    real dt, eps, big;
+};
+hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
+
+struct P2Args {
+    int nl;
+    const int *nlev_nod;
+    const int *nodes;   // node list to process (nullptr = 0..count-1)
+    int count;
+    const real *plus, *minus, *ttf, *LO, *hnode, *hnode_new, *area;
+    real *adf_v, *adf_h, *del_v, *del_h;
+    real dt;
+};
+hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
+
+// Stepwise kernels, one per reference step.
+hipError_t launch_a1(int n_nodes, int nl, const int *nlev_nod, const real *LO, const real *ttf,
+                     real *tmax, real *tmin, hipStream_t s);
+hipError_t launch_a2(int n_elem, int nl, const int *nlev_elem, const int *elem2D_nodes,
+                     const real *tmax, const real *tmin, real *UV, real big, hipStream_t s);
+hipError_t launch_a3(int n_owned, int nl, int vlimit, const int *nlev_nod, const int *nie,
+                     const int *nie_num, int dim, const real *UV, const real *LO, real *tmax,
+                     real *tmin, hipStream_t s);
+hipError_t launch_b1v(int n_owned, int nl, const int *nlev_nod, const real *adf_v, real *plus,
+                      real *minus, hipStream_t s);
+hipError_t launch_b1h(const MeshPlanDev &mp, int nl, const real *adf_h, real *plus, real *minus,
+                      hipStream_t s);
+hipError_t launch_b2(int n_owned, int nl, const int *nlev_nod, const real *area_inv,
+                     const real *tmax, const real *tmin, real *plus, real *minus, real dt,
+                     real eps, hipStream_t s);
+hipError_t launch_b3v(int n_owned, int nl, const int *nlev_nod, const real *plus,
+                      const real *minus, real *adf_v, hipStream_t s);
+hipError_t launch_b3h(int n_edges, int nl, const int *nlev_elem, const int *edges,
+                      const int *edge_tri, const real *plus, const real *minus, real *adf_h,
+                      hipStream_t s);
+hipError_t launch_b3h_list(const int *edge_list, int count, int nl, const int *nlev_elem,
+                           const int *edges, const int *edge_tri, const real *plus,
+                           const real *minus, real *adf_h, hipStream_t s);
+hipError_t launch_cv(int n_owned, int nl, const int *nlev_nod, const real *ttf, const real *hnode,
+                     const real *LO, const real *hnode_new, const real *adf_v, const real *area,
+                     real *del_v, real dt, hipStream_t s);
+hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const real *area,
+                     real *del_h, real dt, hipStream_t s);
+
+// Halo pack / unpack of (plus, minus) columns.
+hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,
+                            const real *minus, real *buf, hipStream_t s);
+hipError_t launch_halo_unpack(const int *nodes, int count, int L, const real *buf, real *plus,
+                              real *minus, hipStream_t s);
+
+}  // namespace f2a

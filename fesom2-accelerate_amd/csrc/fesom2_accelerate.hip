@@ -1,0 +1,424 @@
+// fesom2_accelerate.hip -- the C-ABI of libfesom2-accelerate.so: memory/stream entry points and the
+// FCT-ALE phases.
+//
+// Mirrors the reference's host layer (src/fesom2-accelerate.cu:17-379): opaque buffer handles,
+// streams and events, and the three phase entry points around the MPI halo exchange, plus the
+// additions declared in include/fesom2-accelerate.h (c-step, fused phase 2, resident mode).
+// Unlike the reference it validates every handle and mesh index on the host before a kernel can
+// touch it, checks every launch, and never computes anything on the CPU.
+#include "f2a_host.hpp"
+
+#include <cstdio>
+#include <cstdlib>
+#include <initializer_list>
+
+using namespace f2a;
+
+
+extern "C" {
+
+void set_mpi_rank_(int *rank, int *total_ranks)
+{
+    // reference src/fesom2-accelerate.cu:206-228
+    const int rank_on_node = (*total_ranks > 0) ? (*rank) % (*total_ranks) : *rank;
+    int count = 0;
+    if (!ok(hipGetDeviceCount(&count), "hipGetDeviceCount")) return;
+    if (count < 1) {
+        report("no HIP devices found on the node where rank %d runs", *rank);
+        return;
+    }
+    const int dev = rank_on_node % count;
+    if (!ok(hipSetDevice(dev), "hipSetDevice")) report("error in setting device id to %d", dev);
+}
+
+void transfer_mesh_(void **ret, int *host_ptr, int *size, int *istat)
+{
+    Buffer *m = allocate(host_ptr, (size_t)(*size) * sizeof(int), false);
+    if (m && h2d(m, true, nullptr, false)) {
+        *ret = m;
+        *istat = 0;
+    } else {
+        *ret = nullptr;
+        *istat = 1;
+    }
+}
+
+void alloc_var_(void **ret, real *host_ptr, int *size, bool *create_event, int *istat)
+{
+    Buffer *m = allocate(host_ptr, (size_t)(*size) * sizeof(real), create_event && *create_event);
+    *istat = m ? 0 : 1;
+    *ret = m;
+}
+
+void reserve_var_(void **ret, int *size, bool *create_event, int *istat)
+{
+    Buffer *m = allocate(nullptr, (size_t)(*size) * sizeof(real), create_event && *create_event);
+    *istat = m ? 0 : 1;
+    *ret = m;
+}
+
+void allocate_pinned_doubles_(void **hostptr, int *size, int *istat)
+{
+    *istat = 0;
+    if (!ok(hipHostMalloc(hostptr, sizeof(real) * (size_t)(*size), hipHostMallocDefault), "hipHostMalloc")) {
+        fprintf(stderr, "fesom2-accelerate: error in allocating page-locked memory, using normal malloc...\n");
+        *hostptr = malloc(sizeof(real) * (size_t)(*size));
+        *istat = 1;
+    }
+}
+
+void transfer_var_(void **mem, real *host_ptr)
+{
+    Buffer *b = buf(mem, "transfer_var_");
+    if (!b) return;
+    b->host_pointer = host_ptr;
+    h2d(b, true, nullptr, false);
+}
+
+void transfer_var_async_(void **mem, real *host_ptr, void **stream, bool *record_event)
+{
+    Buffer *b = buf(mem, "transfer_var_async_");
+    if (!b) return;
+    b->host_pointer = host_ptr;
+    h2d(b, false, stream_of(stream), record_event && *record_event);
+}
+
+void make_stream_(void **stream, int *istat)
+{
+    *istat = 0;
+    auto *s = new hipStream_t;
+    if (!ok(hipStreamCreate(s), "hipStreamCreate")) {
+        *istat = 1;
+        fprintf(stderr, "fesom2-accelerate: error in creating HIP stream... returning default stream\n");
+        *s = nullptr;
+    }
+    *stream = s;
+}
+
+void await_stream_(void **s, int *istat)
+{
+    *istat = ok(hipStreamSynchronize(stream_of(s)), "hipStreamSynchronize") ? 0 : 1;
+}
+
+// ----------------------------------------------------------------------------- phase 1
+
+void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **fct_ttf_min,
+                           void **fct_plus, void **fct_minus, void **ttf, void **fct_LO,
+                           void **fct_adf_v, void **fct_adf_h, void **UV_rhs, void **area_inv,
+                           int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
+                           int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                           void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                           void **nod2D_edges, void **elem2D_edges, int *vlimit, real *flux_eps,
+                           real *bignumber, real *dt)
+{
+    *alg_state = 0;
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = *myDim_nod2D + *eDim_nod2D, T = *myDim_elem2D, E = *myDim_edge2D;
+    const int NL = *nl, L = NL - 1;
+    if (!check_levels(NL, "fct_ale_pre_comm_acc_")) return;
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = need(nlevels_elem2D, sizeof(int) * (size_t)T, "nlevels_elem2D");
+    Buffer *bnlnod = need(nlevels_nod2D, sizeof(int) * (size_t)NT, "nlevels_nod2D");
+    mh.elem_nodes = need(elem2D_nodes, 3 * sizeof(int) * (size_t)T, "elem2D_nodes");
+    mh.nie = buf(nod_in_elem2D, "nod_in_elem2D");
+    mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
+    mh.dim = *nod_in_elem2D_dim;
+    Buffer *bmax = buf(fct_ttf_max, "fct_ttf_max"), *bmin = buf(fct_ttf_min, "fct_ttf_min");
+    Buffer *bplus = need(fct_plus, col_bytes(N, L), "fct_plus");
+    Buffer *bminus = need(fct_minus, col_bytes(N, L), "fct_minus");
+    Buffer *bttf = need(ttf, col_bytes(NT, L), "ttf");
+    Buffer *blo = need(fct_LO, col_bytes(NT, L), "fct_LO");
+    Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L), "fct_adf_h");
+    Buffer *buv = buf(UV_rhs, "UV_rhs");
+    Buffer *bainv = need(area_inv, col_bytes(N, NL), "area_inv");
+    if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie ||
+        !mh.nie_num || !bmax || !bmin || !bplus || !bminus || !bttf || !blo || !badfv || !badfh ||
+        !buv || !bainv)
+        return;
+    const bool stepwise = kernel_path() == 1;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, !stepwise);
+    if (!plan) return;
+
+    if (!g_resident && !h2d(blo, false, st, false)) return;  // reference :268
+    const int *nlev_nod = dptr<int>(bnlnod);
+    wait_event(bttf, st);  // reference :293 ("ttf: transferred before fct_ale_muscl_LH")
+    wait_event(badfv, st);
+    wait_event(badfh, st);
+
+    auto finish = [&](int state, std::initializer_list<Buffer *> outs) {
+        *alg_state = state;
+        if (!g_resident)
+            for (Buffer *b : outs)
+                if (!d2h_async(b, st)) {
+                    *alg_state = 0;  // reference transfer_back :249-253
+                    return;
+                }
+    };
+
+    if (!stepwise) {
+        f2a::P1Args a{N, NL, *vlimit, nlev_nod, dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
+                      dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
+                      *dt, *flux_eps, *bignumber};
+        if (!ok(f2a::launch_p1_fused(plan->dev, a, st), "fct_ale_p1")) return;
+        finish(6, {bplus, bminus});
+        return;
+    }
+
+    // stepwise path: one kernel per reference step, reference alg_state numbering (:294-337)
+    if (!need(fct_ttf_max, col_bytes(NT, L), "fct_ttf_max") || !need(fct_ttf_min, col_bytes(NT, L), "fct_ttf_min") ||
+        !need(UV_rhs, col_bytes(T, 2 * L), "UV_rhs") || mh.nie->size < sizeof(int) * (size_t)mh.dim * N ||
+        mh.nie_num->size < sizeof(int) * (size_t)N) {
+        report("fct_ale_pre_comm_acc_: scratch or nod_in_elem2D handles too small");
+        return;
+    }
+    const int limit = num_kernels_limit();
+    real *tmax = dptr<real>(bmax), *tmin = dptr<real>(bmin);
+    if (!ok(f2a::launch_a1(NT, NL, nlev_nod, dptr<real>(blo), dptr<real>(bttf), tmax, tmin, st), "fct_ale_a1")) return;
+    if (limit < 2) return finish(1, {bmax, bmin});
+    if (!ok(f2a::launch_a2(T, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.elem_nodes), tmax, tmin, dptr<real>(buv), *bignumber, st), "fct_ale_a2"))
+        return;
+    if (limit < 3) return finish(2, {bmax, bmin, buv});
+    if (!ok(f2a::launch_a3(N, NL, *vlimit, nlev_nod, dptr<int>(mh.nie), dptr<int>(mh.nie_num), mh.dim,
+                           dptr<real>(buv), dptr<real>(blo), tmax, tmin, st), "fct_ale_a3"))
+        return;
+    if (limit < 4) return finish(3, {bmax, bmin});
+    if (!ok(f2a::launch_b1v(N, NL, nlev_nod, dptr<real>(badfv), dptr<real>(bplus), dptr<real>(bminus), st), "fct_ale_b1_vertical"))
+        return;
+    if (limit < 5) return finish(4, {bmax, bmin, bplus, bminus});
+    if (!ok(f2a::launch_b1h(plan->dev, NL, dptr<real>(badfh), dptr<real>(bplus), dptr<real>(bminus), st), "fct_ale_b1_horizontal"))
+        return;
+    if (limit < 6) return finish(5, {bmax, bmin, bplus, bminus});
+    if (!ok(f2a::launch_b2(N, NL, nlev_nod, dptr<real>(bainv), tmax, tmin, dptr<real>(bplus), dptr<real>(bminus), *dt, *flux_eps, st),
+            "fct_ale_b2"))
+        return;
+    finish(6, {bplus, bminus});
+}
+
+// ----------------------------------------------------------------------------- phase 2
+
+void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                             void **fct_adf_v, int *myDim_nod2D, int *nl, void **nlevels_nod2D)
+{
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NL = *nl, L = NL - 1;
+    if (!check_levels(NL, "fct_ale_inter_comm_acc_")) return;
+    Buffer *bplus = need(fct_plus, col_bytes(N, L), "fct_plus"), *bminus = need(fct_minus, col_bytes(N, L), "fct_minus");
+    Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v");
+    Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    if (!bplus || !bminus || !badfv || !bnl) return;
+    if (!ok(f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st), "fct_ale_b3_vertical"))
+        return;
+    *alg_state = 7;
+    if (!g_resident && !d2h_async(badfv, st)) *alg_state = 0;
+}
+
+void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                            void **fct_adf_h, int *myDim_edge2D, int *nl, void **nlevels_elem2D,
+                            int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges)
+{
+    (void)nod_in_elem2D_dim;
+    const hipStream_t st = stream_of(s);
+    const int E = *myDim_edge2D, NL = *nl, L = NL - 1;
+    if (!check_levels(NL, "fct_ale_post_comm_acc_")) return;
+    Buffer *bplus = buf(fct_plus, "fct_plus"), *bminus = buf(fct_minus, "fct_minus");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L), "fct_adf_h");
+    Buffer *bnle = buf(nlevels_elem2D, "nlevels_elem2D");
+    Buffer *bed = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    Buffer *bet = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    if (!bplus || !bminus || !badfh || !bnle || !bed || !bet) return;
+    // Index validation (every edge node within the plus/minus columns) comes from the edge plan.
+    MeshHandles mh;
+    mh.edges = bed;
+    mh.edge_tri = bet;
+    mh.nlev_elem = bnle;
+    const int ncols = (int)(std::min(bplus->size, bminus->size) / ((size_t)L * sizeof(real)));
+    const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
+    if (!plan) return;
+    if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
+    if (!ok(f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus), dptr<real>(bminus),
+                            dptr<real>(badfh), st),
+            "fct_ale_b3_horizontal"))
+        return;
+    *alg_state = 8;
+    if (!g_resident && !d2h_async(badfh, st)) *alg_state = 0;
+}
+
+void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del_ttf_advhoriz,
+                    void **ttf, void **fct_LO, void **hnode, void **hnode_new, void **fct_adf_v,
+                    void **fct_adf_h, void **area, int *myDim_nod2D, int *eDim_nod2D,
+                    int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                    void **nod2D_edges, void **elem2D_edges, real *dt)
+{
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
+    if (!check_levels(NL, "fct_ale_c_acc_")) return;
+    Buffer *bdv = need(del_ttf_advvert, col_bytes(N, L), "del_ttf_advvert");
+    Buffer *bdh = need(del_ttf_advhoriz, col_bytes(N, L), "del_ttf_advhoriz");
+    Buffer *bttf = need(ttf, col_bytes(N, L), "ttf"), *blo = need(fct_LO, col_bytes(N, L), "fct_LO");
+    Buffer *bh = need(hnode, col_bytes(N, L), "hnode"), *bhn = need(hnode_new, col_bytes(N, L), "hnode_new");
+    Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v"), *badfh = need(fct_adf_h, col_bytes(E, L), "fct_adf_h");
+    Buffer *barea = need(area, col_bytes(N, NL), "area");
+    Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    if (!bdv || !bdh || !bttf || !blo || !bh || !bhn || !badfv || !badfh || !barea || !bnl || !mh.edges || !mh.edge_tri || !mh.nlev_elem)
+        return;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    if (!plan) return;
+    if (!ok(f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
+                           dptr<real>(badfv), dptr<real>(barea), dptr<real>(bdv), *dt, st),
+            "fct_ale_c_vertical"))
+        return;
+    if (!ok(f2a::launch_ch(plan->dev, NL, dptr<real>(badfh), dptr<real>(barea), dptr<real>(bdh), *dt, st), "fct_ale_c_horizontal"))
+        return;
+    *alg_state = 9;
+    if (!g_resident && (!d2h_async(bdv, st) || !d2h_async(bdh, st))) *alg_state = 0;
+}
+
+void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                              void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
+                              void **del_ttf_advhoriz, void **ttf, void **fct_LO, void **hnode,
+                              void **hnode_new, void **area, int *myDim_nod2D, int *eDim_nod2D,
+                              int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                              real *dt)
+{
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
+    if (!check_levels(NL, "fct_ale_post_comm_c_acc_")) return;
+    Buffer *bplus = need(fct_plus, col_bytes(NT, L), "fct_plus"), *bminus = need(fct_minus, col_bytes(NT, L), "fct_minus");
+    Buffer *bdv = need(del_ttf_advvert, col_bytes(N, L), "del_ttf_advvert");
+    Buffer *bdh = need(del_ttf_advhoriz, col_bytes(N, L), "del_ttf_advhoriz");
+    Buffer *bttf = need(ttf, col_bytes(N, L), "ttf"), *blo = need(fct_LO, col_bytes(N, L), "fct_LO");
+    Buffer *bh = need(hnode, col_bytes(N, L), "hnode"), *bhn = need(hnode_new, col_bytes(N, L), "hnode_new");
+    Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v"), *badfh = need(fct_adf_h, col_bytes(E, L), "fct_adf_h");
+    Buffer *barea = need(area, col_bytes(N, NL), "area");
+    Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    if (!bplus || !bminus || !bdv || !bdh || !bttf || !blo || !bh || !bhn || !badfv || !badfh || !barea || !bnl ||
+        !mh.edges || !mh.edge_tri || !mh.nlev_elem)
+        return;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    if (!plan) return;
+    if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
+    if (!ok(f2a::launch_b3h(E, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.edges), dptr<int>(mh.edge_tri), dptr<real>(bplus),
+                            dptr<real>(bminus), dptr<real>(badfh), st),
+            "fct_ale_b3_horizontal"))
+        return;
+    *alg_state = 8;
+    f2a::P2Args a{NL, dptr<int>(bnl), nullptr, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
+                  dptr<real>(blo), dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv),
+                  dptr<real>(badfh), dptr<real>(bdv), dptr<real>(bdh), *dt};
+    if (!ok(f2a::launch_p2_fused(plan->dev, a, st), "fct_ale_p2")) return;
+    *alg_state = 9;
+    if (!g_resident)
+        for (Buffer *b : {badfv, badfh, bdv, bdh})
+            if (!d2h_async(b, st)) {
+                *alg_state = 0;
+                return;
+            }
+}
+
+// ----------------------------------------------------------------------------- utilities
+
+void fesom2_set_resident_(int *resident) { g_resident = (resident && *resident) ? 1 : 0; }
+void fesom2_set_path_(int *path) { set_kernel_path(path ? *path : 0); }
+
+void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D,
+                          int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                          void **elem2D_nodes, void **nod_in_elem2D_num, void **nod_in_elem2D,
+                          int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges)
+{
+    *istat = 1;
+    (void)myDim_elem2D;
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D;
+    MeshHandles mh;
+    mh.edges = buf(nod2D_edges, "nod2D_edges");
+    mh.edge_tri = buf(elem2D_edges, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    Buffer *bnlnod = buf(nlevels_nod2D, "nlevels_nod2D");
+    mh.elem_nodes = buf(elem2D_nodes, "elem2D_nodes");
+    mh.nie = buf(nod_in_elem2D, "nod_in_elem2D");
+    mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
+    mh.dim = *nod_in_elem2D_dim;
+    if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
+    if (get_plan(mh, N, NT, E, *nl, true) && get_plan(mh, N, NT, E, *nl, false)) *istat = 0;
+}
+
+void fesom2_download_(void **mem, void *host_ptr, int *istat)
+{
+    Buffer *b = buf(mem, "fesom2_download_");
+    *istat = (b && ok(hipMemcpy(host_ptr, b->device_pointer, b->size, hipMemcpyDeviceToHost), "D2H")) ? 0 : 1;
+}
+
+void fesom2_upload_(void **mem, void *host_ptr, int *istat)
+{
+    Buffer *b = buf(mem, "fesom2_upload_");
+    *istat = (b && ok(hipMemcpy(b->device_pointer, host_ptr, b->size, hipMemcpyHostToDevice), "H2D")) ? 0 : 1;
+}
+
+void fesom2_free_(void **mem)
+{
+    Buffer *b = buf(mem, "fesom2_free_");
+    if (!b) return;
+    drop_plans_of(b);
+    (void)hipFree(b->device_pointer);
+    if (b->has_event) (void)hipEventDestroy(b->event);
+    b->magic = 0;
+    delete b;
+    *mem = nullptr;
+}
+
+void fesom2_free_stream_(void **stream)
+{
+    if (!stream || !*stream) return;
+    auto *s = static_cast<hipStream_t *>(*stream);
+    if (*s) (void)hipStreamDestroy(*s);
+    delete s;
+    *stream = nullptr;
+}
+
+void fesom2_free_pinned_(void **hostptr)
+{
+    if (hostptr && *hostptr) (void)hipHostFree(*hostptr);
+    if (hostptr) *hostptr = nullptr;
+}
+
+void fesom2_device_sync_(int *istat) { *istat = ok(hipDeviceSynchronize(), "hipDeviceSynchronize") ? 0 : 1; }
+
+const char *fesom2_last_error(void) { return last_error(); }
+
+void fesom2_event_create_(void **ev, int *istat)
+{
+    auto *e = new hipEvent_t;
+    *istat = ok(hipEventCreate(e), "hipEventCreate") ? 0 : 1;
+    *ev = e;
+}
+
+void fesom2_event_record_(void **ev, void **s) { (void)hipEventRecord(*static_cast<hipEvent_t *>(*ev), stream_of(s)); }
+
+void fesom2_event_elapsed_(void **ev0, void **ev1, float *ms)
+{
+    hipEvent_t e0 = *static_cast<hipEvent_t *>(*ev0), e1 = *static_cast<hipEvent_t *>(*ev1);
+    (void)hipEventSynchronize(e1);
+    if (!ok(hipEventElapsedTime(ms, e0, e1), "hipEventElapsedTime")) *ms = -1.f;
+}
+
+void fesom2_event_free_(void **ev)
+{
+    if (!ev || !*ev) return;
+    auto *e = static_cast<hipEvent_t *>(*ev);
+    (void)hipEventDestroy(*e);
+    delete e;
+    *ev = nullptr;
+}
+
+}  // extern "C"

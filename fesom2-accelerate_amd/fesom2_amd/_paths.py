@@ -1,0 +1,14 @@
+"""Locate the in-tree shared libraries (built by ``make -C fesom2-accelerate_amd``)."""
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # fesom2-accelerate_amd/
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+
+
+def lib_path(name):
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{name} is not built ({path}); run `make -C fesom2-accelerate_amd` or __graft_entry__.build()")
+    return path

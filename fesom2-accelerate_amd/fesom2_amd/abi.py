@@ -1,0 +1,146 @@
+"""ctypes bindings of ``libfesom2-accelerate.so`` -- exactly the C-ABI of include/fesom2-accelerate.h.
+
+This is the binding a maintainer of the reference's Python/kernel_tuner harness would use (the
+reference declares the same entry points at ``include/fesom2-accelerate.h:128-236``).  Every
+argument is passed by pointer, as gfortran does; device buffers are opaque ``void*`` handles
+passed as ``void**``.
+
+Loading fails loudly when the library is missing: there is no fallback path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._paths import lib_path
+
+# every exported symbol of include/fesom2-accelerate.h (checked by tests/test_abi.py)
+EXPORTS = (
+    "set_mpi_rank_", "transfer_mesh_", "alloc_var_", "reserve_var_", "allocate_pinned_doubles_",
+    "transfer_var_", "transfer_var_async_", "make_stream_", "await_stream_",
+    "fct_ale_pre_comm_acc_", "fct_ale_inter_comm_acc_", "fct_ale_post_comm_acc_",
+    "fct_ale_a1_reference_", "fct_ale_a2_reference_", "fct_ale_a3_reference_", "fct_ale_a4_reference_",
+    "fct_ale_pre_comm_",
+    "fct_ale_c_acc_", "fct_ale_post_comm_c_acc_", "fesom2_set_resident_", "fesom2_set_path_",
+    "fesom2_prepare_mesh_", "fesom2_download_", "fesom2_upload_", "fesom2_free_", "fesom2_free_stream_",
+    "fesom2_free_pinned_", "fesom2_device_sync_", "fesom2_last_error", "fesom2_event_create_",
+    "fesom2_event_record_", "fesom2_event_elapsed_", "fesom2_event_free_",
+    "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_halo_plan_",
+    "fesom2_halo_plan_free_", "fct_ale_exchange_acc_",
+)
+
+_dll = None
+
+
+def dll():
+    """The engine library (loaded once)."""
+    global _dll
+    if _dll is None:
+        _dll = C.CDLL(lib_path("libfesom2-accelerate.so"))
+        _dll.fesom2_last_error.restype = C.c_char_p
+    return _dll
+
+
+def ip(v):
+    """int* argument."""
+    return C.byref(C.c_int(int(v)))
+
+
+def dp(v):
+    """double* argument."""
+    return C.byref(C.c_double(float(v)))
+
+
+def bp(v):
+    """bool* argument (C99 _Bool / Fortran logical(c_bool))."""
+    return C.byref(C.c_bool(bool(v)))
+
+
+def arr(a):
+    """host array argument (numpy, contiguous)."""
+    assert a.flags.c_contiguous, "host arrays must be contiguous"
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def last_error():
+    return dll().fesom2_last_error().decode()
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def check(istat, what):
+    v = istat.value if hasattr(istat, "value") else istat
+    if v != 0:
+        raise HipError(f"{what} failed (istat={v}): {last_error()}")
+
+
+class Handle:
+    """A ``void*`` returned by the library; ``ref`` is the ``void**`` the entry points take."""
+
+    def __init__(self, name=""):
+        self.ptr = C.c_void_p()
+        self.name = name
+
+    @property
+    def ref(self):
+        return C.byref(self.ptr)
+
+    def __bool__(self):
+        return bool(self.ptr.value)
+
+
+class Stream(Handle):
+    def __init__(self):
+        super().__init__("stream")
+        st = C.c_int(0)
+        dll().make_stream_(self.ref, C.byref(st))
+        if st.value:
+            raise HipError(f"make_stream_ fell back to the null stream: {last_error()}")
+
+    def sync(self):
+        st = C.c_int(0)
+        dll().await_stream_(self.ref, C.byref(st))
+        check(st, "await_stream_")
+
+    def free(self):
+        if self:
+            dll().fesom2_free_stream_(self.ref)
+
+
+class Event(Handle):
+    def __init__(self):
+        super().__init__("event")
+        st = C.c_int(0)
+        dll().fesom2_event_create_(self.ref, C.byref(st))
+        check(st, "fesom2_event_create_")
+
+    def record(self, stream):
+        dll().fesom2_event_record_(self.ref, stream.ref)
+
+    def elapsed_ms(self, later):
+        ms = C.c_float(0)
+        dll().fesom2_event_elapsed_(self.ref, later.ref, C.byref(ms))
+        return ms.value
+
+    def free(self):
+        if self:
+            dll().fesom2_event_free_(self.ref)
+
+
+def set_resident(on):
+    dll().fesom2_set_resident_(ip(1 if on else 0))
+
+
+def set_path(path):
+    dll().fesom2_set_path_(ip(1 if path in ("stepwise", 1) else 0))
+
+
+def device_sync():
+    st = C.c_int(0)
+    dll().fesom2_device_sync_(C.byref(st))
+    check(st, "fesom2_device_sync_")
+
+
+def set_mpi_rank(rank, nranks):
+    dll().set_mpi_rank_(ip(rank), ip(nranks))

@@ -1,0 +1,182 @@
+"""Host driver: issues the C-ABI calls in the order FESOM2's Fortran ``fct_ale`` does.
+
+Call sequence (reference ``src/fesom2-accelerate.cu``)::
+
+    transfer_mesh_ x7                      once per mesh      (:114-127)
+    alloc_var_ / reserve_var_              once per field     (:129-141)
+    transfer_var_async_(ttf, adf_v, adf_h) per step, events   (:163-168, waited on at :293/:316/:326)
+    fct_ale_pre_comm_acc_                  a1..b2             (:258-340)
+    [exchange_nod(fct_plus, fct_minus)]    host MPI, or fct_ale_exchange_acc_ (RCCL) here
+    fct_ale_inter_comm_acc_                b3-vertical        (:342-356)
+    fct_ale_post_comm_acc_                 b3-horizontal      (:358-379)
+    fct_ale_c_acc_                         c-step (new; the reference leaves it to Fortran)
+
+or, fused: ``fct_ale_pre_comm_acc_`` -> exchange -> ``fct_ale_post_comm_c_acc_``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .abi import arr, bp, check, dll, dp, ip
+
+MESH_ARRAYS = ("nlev_nod", "nlev_elem", "elem2D_nodes", "nie_num", "nie", "edges", "edge_tri")
+NODE_FIELDS = ("ttf", "LO", "hnode", "hnode_new", "del_v", "del_h", "plus", "minus")
+NL_FIELDS = ("adf_v", "area", "area_inv")
+
+
+class DeviceMesh:
+    """Mesh connectivity uploaded with ``transfer_mesh_`` (int32, 1-based)."""
+
+    def __init__(self, m):
+        self.m = m
+        self.h = {}
+        self._host = {}
+        for name in MESH_ARRAYS:
+            a = np.ascontiguousarray(getattr(m, name), dtype=np.int32)
+            self._host[name] = a  # the library keeps the host pointer, like Fortran's arrays
+            h = abi.Handle(name)
+            st = C.c_int(0)
+            dll().transfer_mesh_(h.ref, arr(a), ip(max(a.size, 1)), C.byref(st))
+            check(st, f"transfer_mesh_({name})")
+            self.h[name] = h
+
+    def prepare(self):
+        m, h = self.m, self.h
+        st = C.c_int(0)
+        dll().fesom2_prepare_mesh_(C.byref(st), ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), h["nlev_nod"].ref,
+                                   h["nlev_elem"].ref, h["elem2D_nodes"].ref, h["nie_num"].ref, h["nie"].ref,
+                                   ip(m.dim), h["edges"].ref, h["edge_tri"].ref)
+        check(st, "fesom2_prepare_mesh_")
+
+    def free(self):
+        for h in self.h.values():
+            if h:
+                dll().fesom2_free_(h.ref)
+        self.h = {}
+
+
+class FctAle:
+    """Device state of one tracer on one (local) mesh, driven through the C-ABI.
+
+    ``fields`` is the dict made by :func:`fesom2_amd.synth.make_fields` (host arrays, kept alive
+    and bound as the handles' host pointers exactly like the Fortran arrays would be).
+    """
+
+    def __init__(self, dmesh: DeviceMesh, fields, stream=None, vlimit=1, flux_eps=1e-16, bignumber=1e3,
+                 dt=1.0):
+        m = dmesh.m
+        self.dm, self.m = dmesh, m
+        self.stream = stream or abi.Stream()
+        self.vlimit, self.eps, self.big, self.dt = vlimit, flux_eps, bignumber, dt
+        NT, L, nl = m.N + m.H, m.L, m.nl
+        self.host = {k: np.ascontiguousarray(v, dtype=np.float64).copy() for k, v in fields.items()}
+        self.host.setdefault("plus", np.zeros(NT * L))
+        self.host.setdefault("minus", np.zeros(NT * L))
+        self.h = {}
+        sizes = {k: NT * L for k in NODE_FIELDS}
+        sizes.update({k: NT * nl for k in NL_FIELDS})
+        sizes["adf_h"] = m.E * L
+        events = {"ttf", "adf_v", "adf_h"}  # the buffers the reference waits on (:293, :316, :326)
+        for name, n in sizes.items():
+            a = self.host[name]
+            assert a.size == n, (name, a.size, n)
+            h = abi.Handle(name)
+            st = C.c_int(0)
+            dll().alloc_var_(h.ref, arr(a), ip(n), bp(name in events), C.byref(st))
+            check(st, f"alloc_var_({name})")
+            self.h[name] = h
+            dll().transfer_var_(h.ref, arr(a))
+        for name, n in (("ttf_max", NT * L), ("ttf_min", NT * L), ("UV_rhs", 2 * L * m.T)):
+            h = abi.Handle(name)
+            st = C.c_int(0)
+            dll().reserve_var_(h.ref, ip(max(n, 1)), bp(False), C.byref(st))
+            check(st, f"reserve_var_({name})")
+            self.h[name] = h
+
+    # ------------------------------------------------------------------ phases (reference names)
+    def pre_comm(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_pre_comm_acc_(
+            C.byref(st), self.stream.ref, h["ttf_max"].ref, h["ttf_min"].ref, h["plus"].ref, h["minus"].ref,
+            h["ttf"].ref, h["LO"].ref, h["adf_v"].ref, h["adf_h"].ref, h["UV_rhs"].ref, h["area_inv"].ref,
+            ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
+            d["elem2D_nodes"].ref, d["nie_num"].ref, d["nie"].ref, ip(m.dim), d["edges"].ref, d["edge_tri"].ref,
+            ip(self.vlimit), dp(self.eps), dp(self.big), dp(self.dt))
+        return st.value
+
+    def inter_comm(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_inter_comm_acc_(C.byref(st), self.stream.ref, h["plus"].ref, h["minus"].ref, h["adf_v"].ref,
+                                      ip(m.N), ip(m.nl), d["nlev_nod"].ref)
+        return st.value
+
+    def post_comm(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_post_comm_acc_(C.byref(st), self.stream.ref, h["plus"].ref, h["minus"].ref, h["adf_h"].ref,
+                                     ip(m.E), ip(m.nl), d["nlev_elem"].ref, ip(m.dim), d["edges"].ref,
+                                     d["edge_tri"].ref)
+        return st.value
+
+    def c_step(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_c_acc_(C.byref(st), self.stream.ref, h["del_v"].ref, h["del_h"].ref, h["ttf"].ref, h["LO"].ref,
+                             h["hnode"].ref, h["hnode_new"].ref, h["adf_v"].ref, h["adf_h"].ref, h["area"].ref,
+                             ip(m.N), ip(m.H), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
+                             d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
+        return st.value
+
+    def post_comm_c(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_post_comm_c_acc_(
+            C.byref(st), self.stream.ref, h["plus"].ref, h["minus"].ref, h["adf_v"].ref, h["adf_h"].ref,
+            h["del_v"].ref, h["del_h"].ref, h["ttf"].ref, h["LO"].ref, h["hnode"].ref, h["hnode_new"].ref,
+            h["area"].ref, ip(m.N), ip(m.H), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
+            d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
+        return st.value
+
+    def full_pass(self, fused=True):
+        """Single-domain pass (no halo): returns the final alg_state (9 on success)."""
+        s1 = self.pre_comm()
+        if s1 != 6:
+            return s1
+        if fused:
+            return self.post_comm_c()
+        s2 = self.inter_comm()
+        s3 = self.post_comm()
+        s4 = self.c_step()
+        return s4 if (s2, s3) == (7, 8) else min(s2, s3)
+
+    # ------------------------------------------------------------------ data movement
+    def upload(self, name, a=None):
+        a = self.host[name] if a is None else np.ascontiguousarray(a, dtype=np.float64)
+        st = C.c_int(0)
+        dll().fesom2_upload_(self.h[name].ref, arr(a), C.byref(st))
+        check(st, f"upload {name}")
+
+    def download(self, name, dtype=np.float64):
+        b = self.h[name]
+        n = {"UV_rhs": 2 * self.m.L * self.m.T}.get(name, self.host[name].size if name in self.host else None)
+        if n is None:
+            n = (self.m.N + self.m.H) * self.m.L
+        out = np.empty(max(n, 1), dtype)  # every handle here holds exactly max(n, 1) doubles
+        st = C.c_int(0)
+        dll().fesom2_download_(b.ref, arr(out), C.byref(st))
+        check(st, f"download {name}")
+        return out[:n]
+
+    def sync(self):
+        self.stream.sync()
+
+    def free(self):
+        for h in self.h.values():
+            if h:
+                dll().fesom2_free_(h.ref)
+        self.h = {}

@@ -1,0 +1,175 @@
+"""Deterministic synthetic FESOM-like meshes and fields (ctypes over ``lib/libfesom2_synth.so``).
+
+The reference carries no mesh; its tuning scripts use unseeded random connectivity
+(e.g. ``kernels/fct_ale_b1_horizontal.py:119-123``).  Here a periodic-x structured triangulation
+with FESOM's array conventions is generated in C (``csrc/synth.c``), and every field value is a
+pure function of (seed, field, global index), so a partition regenerates exactly the bits of the
+whole mesh.  Sizes follow SURVEY.md §8 (T ~ 2N, E ~ 3N, dim = 6).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+import os
+
+import numpy as np
+
+from ._paths import lib_path
+
+_synth = None
+
+
+def _lib():
+    global _synth
+    if _synth is None:
+        path = lib_path("libfesom2_synth.so")
+        _synth = C.CDLL(path)
+        _synth.synth_mesh_build.restype = C.c_int
+        _synth.synth_mesh_build.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int] + [C.c_void_p] * 7
+        _synth.synth_fill.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_void_p,
+                                      C.c_double, C.c_double, C.c_void_p]
+    return _synth
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+# configs of BASELINE.json / SURVEY.md §8(d): name -> (nx, ny, nl)
+CONFIGS = {
+    "tiny": (16, 8, 11),
+    "8k x 20": (128, 64, 21),
+    "127k x 47": (512, 248, 48),
+    "1.2M x 80": (1600, 750, 81),
+    "9.6M x 80": (3200, 3000, 81),
+}
+
+FIELD_IDS = dict(ttf=10, LO=11, adf_v=12, adf_h=13, area=14, hnode=15, hnode_new=16, del_v=17, del_h=18)
+
+
+@dataclasses.dataclass
+class Mesh:
+    """One (local) mesh in the reference's argument convention.
+
+    N = myDim_nod2D, H = eDim_nod2D, T = myDim_elem2D, E = myDim_edge2D, nl levels (L = nl-1).
+    Connectivity is int32 and 1-based; node_gid / edge_gid map local to global ids (fields are
+    keyed on global ids).
+    """
+    nl: int
+    N: int
+    H: int
+    T: int
+    E: int
+    dim: int
+    elem2D_nodes: np.ndarray
+    edges: np.ndarray
+    edge_tri: np.ndarray
+    nie_num: np.ndarray
+    nie: np.ndarray
+    nlev_elem: np.ndarray
+    nlev_nod: np.ndarray
+    node_gid: np.ndarray
+    edge_gid: np.ndarray
+    name: str = ""
+
+    @property
+    def L(self):
+        return self.nl - 1
+
+    @property
+    def cells(self):
+        """Cn = sum over owned nodes of (nlevels_nod2D - 1): the wet cells of one pass."""
+        return int(np.sum(self.nlev_nod[: self.N].astype(np.int64) - 1))
+
+    @property
+    def edge_cells(self):
+        """Ce = sum over local edges of max(nl1, nl2)."""
+        t = self.edge_tri.reshape(-1, 2)
+        nl1 = self.nlev_elem[t[:, 0] - 1].astype(np.int64) - 1
+        second = t[:, 1] > 0
+        nl2 = np.where(second, self.nlev_elem[np.maximum(t[:, 1] - 1, 0)].astype(np.int64) - 1, 0)
+        return int(np.sum(np.maximum(nl1, nl2)))
+
+
+def make_mesh(nx, ny, nl, seed=42, full_depth=False, name=""):
+    """Periodic-x structured triangulation with nx*ny nodes (single domain: H = 0)."""
+    N, T, E = nx * ny, 2 * nx * (ny - 1), 3 * nx * (ny - 1) + nx
+    en = np.zeros(3 * T, np.int32)
+    ed = np.zeros(2 * E, np.int32)
+    et = np.zeros(2 * E, np.int32)
+    nn = np.zeros(N, np.int32)
+    nie = np.zeros(6 * N, np.int32)
+    le = np.zeros(T, np.int32)
+    ln = np.zeros(N, np.int32)
+    rc = _lib().synth_mesh_build(nx, ny, nl, seed, 1 if full_depth else 0, _p(en), _p(ed), _p(et),
+                                 _p(nn), _p(nie), _p(le), _p(ln))
+    if rc:
+        raise ValueError(f"synth_mesh_build({nx}, {ny}, {nl}) rejected the sizes")
+    return Mesh(nl=nl, N=N, H=0, T=T, E=E, dim=6, elem2D_nodes=en, edges=ed, edge_tri=et, nie_num=nn,
+                nie=nie, nlev_elem=le, nlev_nod=ln, node_gid=np.arange(N, dtype=np.int64),
+                edge_gid=np.arange(E, dtype=np.int64), name=name or f"{nx}x{ny}x{nl - 1}")
+
+
+def config_mesh(name, full_depth=False, seed=42):
+    nx, ny, nl = CONFIGS[name]
+    return make_mesh(nx, ny, nl, seed=seed, full_depth=full_depth, name=name)
+
+
+def fill(seed, field, dist, ncols, stride, gid, a, b):
+    out = np.empty(int(ncols) * int(stride), np.float64)
+    g = None if gid is None else np.ascontiguousarray(gid, dtype=np.int64)
+    _lib().synth_fill(seed, FIELD_IDS[field] if isinstance(field, str) else field, dist, int(ncols), int(stride),
+                      None if g is None else _p(g), a, b, _p(out))
+    return out
+
+
+def make_fields(m: Mesh, seed=43, area_scale=1.0, adf_scale=0.5):
+    """All per-tracer and per-mesh fields of one pass, keyed on global ids.
+
+    Scales keep the limiter active (ratios in b2 of order one) so b2/b3 are exercised.
+    """
+    NT, L, nl = m.N + m.H, m.L, m.nl
+    g = m.node_gid
+    f = {}
+    f["ttf"] = fill(seed, "ttf", 1, NT, L, g, 0.0, 1.0)
+    f["LO"] = fill(seed, "LO", 1, NT, L, g, 0.0, 1.0)
+    adf_v = fill(seed, "adf_v", 1, NT, nl, g, 0.0, adf_scale).reshape(NT, nl)
+    # the bottom flux is always zero (docs/refactoring.md:232)
+    adf_v[np.arange(nl)[None, :] >= (m.nlev_nod[:, None] - 1)] = 0.0
+    f["adf_v"] = adf_v.reshape(-1)
+    f["adf_h"] = fill(seed, "adf_h", 1, m.E, L, m.edge_gid, 0.0, adf_scale)
+    f["area"] = fill(seed, "area", 0, NT, nl, g, 0.5 * area_scale, 2.0 * area_scale)
+    f["area_inv"] = 1.0 / f["area"]
+    f["hnode"] = fill(seed, "hnode", 0, NT, L, g, 5.0, 50.0)
+    f["hnode_new"] = fill(seed, "hnode_new", 0, NT, L, g, 5.0, 50.0)
+    f["del_v"] = fill(seed, "del_v", 1, NT, L, g, 0.0, 1.0)
+    f["del_h"] = fill(seed, "del_h", 1, NT, L, g, 0.0, 1.0)
+    return f
+
+
+def permute_mesh(m: Mesh, seed=7):
+    """Shuffle node, element and edge numbering (an 'unstructured' stress variant).
+
+    Global ids travel with the entities, so fields generated from the result describe the same
+    physical problem; only the memory order changes.
+    """
+    assert m.H == 0
+    rng = np.random.default_rng(seed)
+    pn = rng.permutation(m.N)  # new id of old node i is pn[i]
+    pe = rng.permutation(m.T)
+    pg = rng.permutation(m.E)
+    inv_n, inv_e, inv_g = np.argsort(pn), np.argsort(pe), np.argsort(pg)
+    mapn = lambda a: (pn[a - 1] + 1).astype(np.int32)
+    en = mapn(m.elem2D_nodes.reshape(-1, 3))[inv_e].reshape(-1)
+    ed = mapn(m.edges.reshape(-1, 2))[inv_g].reshape(-1)
+    t = m.edge_tri.reshape(-1, 2)
+    t2 = np.where(t > 0, pe[np.maximum(t - 1, 0)] + 1, 0).astype(np.int32)
+    et = t2[inv_g].reshape(-1)
+    nie = m.nie.reshape(-1, m.dim)
+    nie2 = np.where(nie > 0, pe[np.maximum(nie - 1, 0)] + 1, 0).astype(np.int32)[inv_n].reshape(-1)
+    return dataclasses.replace(
+        m, elem2D_nodes=np.ascontiguousarray(en), edges=np.ascontiguousarray(ed),
+        edge_tri=np.ascontiguousarray(et), nie_num=np.ascontiguousarray(m.nie_num[inv_n]),
+        nie=np.ascontiguousarray(nie2), nlev_elem=np.ascontiguousarray(m.nlev_elem[inv_e]),
+        nlev_nod=np.ascontiguousarray(m.nlev_nod[inv_n]), node_gid=np.ascontiguousarray(m.node_gid[inv_n]),
+        edge_gid=np.ascontiguousarray(m.edge_gid[inv_g]), name=m.name + "+perm")

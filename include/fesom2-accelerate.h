@@ -1,0 +1,170 @@
+/*
+ * fesom2-accelerate.h -- C-ABI of the MI355X-native FCT-ALE engine (libfesom2-accelerate.so).
+ *
+ * Drop-in for the reference's include/fesom2-accelerate.h:128-236 (ESiWACE-S1/fesom2-accelerate).
+ * Every entry point keeps the reference's name, gfortran-style trailing underscore, by-pointer
+ * arguments and meaning; device buffers are opaque handles passed as void** (the caller stores the
+ * void* the library returned).  No CUDA/HIP or C++ types appear in any signature.
+ *
+ * Conventions (reference src/fesom2-accelerate.cu):
+ *   istat      0 ok, 1 failure (message on stderr)
+ *   alg_state  last completed step, for the caller's CPU fallback: pre_comm -> 6,
+ *              inter_comm -> 7, post_comm -> 8 (reference :337, :354, :377); new c-step -> 9.
+ *              vlimit 2/3 are computed on the GPU as well (the reference GPU path ignores vlimit).
+ *   layouts    Fortran column-major: node fields (nl-1, nodes), fct_adf_v/area/area_inv (nl, nodes),
+ *              fct_adf_h (nl-1, edges), UV_rhs (2, nl-1, elem); connectivity int32, 1-based.
+ *   threading  one host thread per rank; all phase work is enqueued on *s; the caller awaits it
+ *              with await_stream_ before touching host outputs.
+ */
+#ifndef FESOM2_ACCELERATE_H
+#define FESOM2_ACCELERATE_H
+
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+typedef double real_type; /* reference .h:10 */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- memory / stream / device */
+
+/* reference .h:146, impl src/fesom2-accelerate.cu:206-228: device = (rank % total_ranks) % ndev */
+void set_mpi_rank_(int *rank, int *total_ranks);
+/* reference .h:147, impl :114-127: allocate + synchronous upload of an int32 array of *size items */
+void transfer_mesh_(void **ret, int *host_ptr, int *size, int *istat);
+/* reference .h:148, impl :129-134: allocate *size doubles bound to host_ptr (no copy) */
+void alloc_var_(void **ret, real_type *host_ptr, int *size, bool *create_event, int *istat);
+/* reference .h:149, impl :136-141: device-only scratch of *size doubles */
+void reserve_var_(void **ret, int *size, bool *create_event, int *istat);
+/* reference .h:150, impl :143-154: pinned host doubles; istat 1 = fell back to malloc */
+void allocate_pinned_doubles_(void **hostptr, int *size, int *istat);
+/* reference .h:151, impl :156-161: rebind host pointer, synchronous H2D */
+void transfer_var_(void **mem, real_type *host_ptr);
+/* reference .h:152, impl :163-168: rebind host pointer, async H2D on *stream, optional event record */
+void transfer_var_async_(void **mem, real_type *host_ptr, void **stream, bool *record_event);
+/* reference .h:153, impl :170-186: heap stream handle; istat 1 = fell back to the null stream */
+void make_stream_(void **stream, int *istat);
+/* reference .h:154, impl :188-198 */
+void await_stream_(void **s, int *istat);
+
+/* ---------------------------------------------------------------- FCT-ALE phases (GPU) */
+
+/* reference .h:156, impl :258-340: a1, a2, a3(+b1-vertical), b1-horizontal, b2; D2H fct_plus/minus */
+void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **fct_ttf_min,
+                           void **fct_plus, void **fct_minus, void **ttf, void **fct_LO,
+                           void **fct_adf_v, void **fct_adf_h, void **UV_rhs, void **area_inv,
+                           int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
+                           int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                           void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                           void **nod2D_edges, void **elem2D_edges, int *vlimit, real_type *flux_eps,
+                           real_type *bignumber, real_type *dt);
+/* reference .h:157, impl :342-356: b3-vertical on owned nodes; D2H fct_adf_v */
+void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                             void **fct_adf_v, int *myDim_nod2D, int *nl, void **nlevels_nod2D);
+/* reference .h:158, impl :358-379: H2D fct_plus/minus (halo filled by the caller's exchange),
+ * b3-horizontal on local edges; D2H fct_adf_h.  The 8th argument holds nlevels(elem): the
+ * reference header names it nlevels_nod2D but its definition (:358) uses nlevels_elem2D. */
+void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                            void **fct_adf_h, int *myDim_edge2D, int *nl, void **nlevels_elem2D,
+                            int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges);
+
+/* ---------------------------------------------------------------- reference CPU-named entries
+ * reference .h:142, :225, :229, :232, :235 (src/reference.cpp:289-438).  Same names and meaning on
+ * host arrays; here they are executed by the GPU engine (stage, launch, copy back, synchronous). */
+void fct_ale_a1_reference_(int *nNodes, int *nLevels_nod2D, int *nl, real_type *fct_ttf_max,
+                           real_type *fct_ttf_min, real_type *fct_low_order, real_type *ttf);
+void fct_ale_a2_reference_(int *nElements, int *nLevels_elem2D, int *nl, real_type *UV_rhs,
+                           int *elem2D_nodes, real_type *fct_ttf_max, real_type *fct_ttf_min,
+                           real_type *bignumber);
+void fct_ale_a3_reference_(int *nNodes2D, int *nLevels_nod2D, int *nl, real_type *fct_ttf_max,
+                           real_type *fct_ttf_min, real_type *fct_LO, real_type *UV_rhs,
+                           real_type *fct_plus, real_type *fct_minus, real_type *fct_adf_v,
+                           int *nod_in_elem2D, int *nod_in_elem2D_num, int *nod_in_elem2D_dim);
+void fct_ale_a4_reference_(int *nNodes2D, int *nLevels_nod2D, int *nLevels_elem2D, int *nl,
+                           int *nEdges2D, real_type *fct_plus, real_type *fct_minus,
+                           real_type *fct_adf_h, real_type *area_inv, real_type *fct_ttf_max,
+                           real_type *fct_ttf_min, int *edges, int *edge_tri, real_type *flux_eps,
+                           real_type *dt);
+void fct_ale_pre_comm_(int *alg_state, real_type *fct_ttf_max, real_type *fct_ttf_min,
+                       real_type *fct_plus, real_type *fct_minus, real_type *ttf, real_type *fct_LO,
+                       real_type *fct_adf_v, real_type *fct_adf_h, real_type *UV_rhs,
+                       real_type *area_inv, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D,
+                       int *myDim_edge2D, int *nl, int *nlevels_nod2D, int *nlevels_elem2D,
+                       int *elem2D_nodes, int *nod_in_elem2D_num, int *nod_in_elem2D,
+                       int *nod_in_elem2D_dim, int *nod2D_edges, int *elem2D_edges, int *vlimit,
+                       real_type *flux_eps, real_type *bignumber, real_type *dt);
+
+/* ================================================================ additions (not in the reference)
+ * Everything below is new API; none of it changes the entry points above. */
+
+/* c-step (docs/refactoring.md:292-314; reference kernels built but never launched):
+ * c-vertical on owned nodes + c-horizontal gathered per owned node; alg_state -> 9. */
+void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del_ttf_advhoriz,
+                    void **ttf, void **fct_LO, void **hnode, void **hnode_new, void **fct_adf_v,
+                    void **fct_adf_h, void **area, int *myDim_nod2D, int *eDim_nod2D,
+                    int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                    void **nod2D_edges, void **elem2D_edges, real_type *dt);
+
+/* Fused phase 2 = b3-vertical + b3-horizontal + c-vertical + c-horizontal in one node-centric pass
+ * (needs fct_plus/minus valid on the halo).  Same results as inter_comm + post_comm + c; alg_state -> 9. */
+void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                              void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
+                              void **del_ttf_advhoriz, void **ttf, void **fct_LO, void **hnode,
+                              void **hnode_new, void **area, int *myDim_nod2D, int *eDim_nod2D,
+                              int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                              real_type *dt);
+
+/* Transfer mode.  0 (default) = reference semantics: pre_comm uploads fct_LO and downloads
+ * fct_plus/minus, inter_comm downloads fct_adf_v, post_comm uploads fct_plus/minus and downloads
+ * fct_adf_h, c downloads del_ttf_*.  1 = device resident: no implicit host transfers. */
+void fesom2_set_resident_(int *resident);
+/* Kernel path.  0 (default) = fused node-centric kernels; 1 = one kernel per reference step
+ * (materialises fct_ttf_max/min and UV_rhs, honours FESOM2_NUM_KERNELS for bisection). */
+void fesom2_set_path_(int *path);
+/* Build the derived mesh structures (edge/ring CSR) ahead of the first pass (otherwise built
+ * lazily, synchronously, on first use). */
+void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D,
+                          int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                          void **elem2D_nodes, void **nod_in_elem2D_num, void **nod_in_elem2D,
+                          int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges);
+/* Copy a handle's device contents to/from a host array (no rebinding), synchronous. */
+void fesom2_download_(void **mem, void *host_ptr, int *istat);
+void fesom2_upload_(void **mem, void *host_ptr, int *istat);
+/* Release a handle / stream / pinned buffer (the reference never frees). */
+void fesom2_free_(void **mem);
+void fesom2_free_stream_(void **stream);
+void fesom2_free_pinned_(void **hostptr);
+/* Device-wide synchronisation and last error string (empty if none). */
+void fesom2_device_sync_(int *istat);
+const char *fesom2_last_error(void);
+/* Timing: create/record/elapsed on a stream (HIP events); used by the benchmark harness. */
+void fesom2_event_create_(void **ev, int *istat);
+void fesom2_event_record_(void **ev, void **s);
+void fesom2_event_elapsed_(void **ev0, void **ev1, float *ms);
+void fesom2_event_free_(void **ev);
+
+/* ---------------------------------------------------------------- multi-GPU halo (RCCL over xGMI)
+ * The reference leaves exchange_nod(fct_plus, fct_minus) to the Fortran host's MPI between
+ * pre_comm and post_comm (docs/refactoring.md:199-200, :235).  This device-resident replacement
+ * packs the owned columns neighbours need, exchanges them with grouped ncclSend/ncclRecv on a
+ * communication stream and unpacks them into the halo columns. */
+void fesom2_comm_unique_id_(char *id128, int *istat);
+void fesom2_comm_init_(void **comm, char *id128, int *rank, int *nranks, int *istat);
+void fesom2_comm_free_(void **comm);
+/* Halo plan: per neighbour rank, the 1-based local node numbers to send (owned) and to receive
+ * (halo), concatenated in neighbour order. */
+void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_counts,
+                       int *send_nodes, int *recv_counts, int *recv_nodes, int *nl, int *istat);
+void fesom2_halo_plan_free_(void **plan);
+/* Exchange fct_plus/fct_minus halo columns; enqueued on *s (work after it on *s sees the halo). */
+void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void **fct_plus,
+                           void **fct_minus);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FESOM2_ACCELERATE_H */

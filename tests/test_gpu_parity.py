@@ -1,0 +1,201 @@
+"""GPU parity: the HIP engine, driven through the C-ABI, against the oracle.
+
+The bar is exact equality (``==`` on every cell, i.e. max-abs error 0, which is inside the
+north star's fp64 tolerance of 1e-12): the engine's edge->node sums are gathers in ascending edge
+order, so they perform the same IEEE additions as reference.cpp, and the library is built with
+-ffp-contract=off.  Meshes are the synthetic ones of SURVEY.md §8(d) (parity levels: element
+levels uniform in [3, nl]; roofline levels: full depth) and a node/element/edge-permuted variant.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_cols_equal
+from fesom2_amd import abi, engine, synth
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    abi.set_mpi_rank(0, 1)
+    abi.set_resident(True)
+    abi.set_path("fused")
+    yield
+    abi.set_resident(False)
+    abi.set_path("fused")
+
+
+_MESHES = {}
+
+
+def mesh(name, full_depth=False, perm=False):
+    key = (name, full_depth, perm)
+    if key not in _MESHES:
+        m = synth.config_mesh(name, full_depth=full_depth)
+        if perm:
+            m = synth.permute_mesh(m)
+        _MESHES[key] = (m, synth.make_fields(m))
+    return _MESHES[key]
+
+
+def run_pass(m, f, fused=True, path="fused", resident=True, vlimit=1):
+    abi.set_resident(resident)
+    abi.set_path(path)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f, vlimit=vlimit)
+    try:
+        st = e.full_pass(fused=fused)
+        e.sync()
+        out = {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        e.free()
+        dm.free()
+        abi.set_resident(True)
+        abi.set_path("fused")
+    return st, out
+
+
+def check_pass(m, got, want):
+    L = m.L
+    assert_cols_equal(got["plus"], want["plus"], m.nlev_nod, L, m.N, "fct_plus")
+    assert_cols_equal(got["minus"], want["minus"], m.nlev_nod, L, m.N, "fct_minus")
+    for k in ("adf_v", "adf_h", "del_v", "del_h"):
+        g, w = got[k], want[k]
+        bad = np.flatnonzero(g != w)
+        assert bad.size == 0, f"{k}: {bad.size} entries differ, first at {bad[:5]}: {g[bad[0]]!r} vs {w[bad[0]]!r}"
+
+
+CASES = [("tiny", False, False), ("8k x 20", False, False), ("8k x 20", True, False),
+         ("8k x 20", False, True), ("127k x 47", False, False)]
+
+
+@pytest.mark.parametrize("name,full,perm", CASES)
+@pytest.mark.parametrize("fused,path", [(True, "fused"), (False, "fused"), (False, "stepwise")])
+def test_full_pass_matches_oracle(name, full, perm, fused, path):
+    m, f = mesh(name, full, perm)
+    want = O.full_pass(m, f)
+    st, got = run_pass(m, f, fused=fused, path=path)
+    assert st == 9
+    check_pass(m, got, want)
+
+
+@pytest.mark.parametrize("vlimit", [2, 3])
+@pytest.mark.parametrize("path", ["fused", "stepwise"])
+def test_vlimit_variants(vlimit, path):
+    """vlimit 2/3 (docs/refactoring.md:113-148), which reference.cpp does not implement."""
+    m, f = mesh("8k x 20")
+    st, want = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
+    assert st == 5
+    abi.set_path(path)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f, vlimit=vlimit)
+    try:
+        assert e.pre_comm() == 6
+        e.sync()
+        assert_cols_equal(e.download("plus"), want["plus"], m.nlev_nod, m.L, m.N, f"plus vlimit {vlimit}")
+        assert_cols_equal(e.download("minus"), want["minus"], m.nlev_nod, m.L, m.N, f"minus vlimit {vlimit}")
+    finally:
+        e.free()
+        dm.free()
+        abi.set_path("fused")
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6])
+def test_stepwise_alg_state_bisection(k, monkeypatch):
+    """FESOM2_NUM_KERNELS=k stops phase 1 after step k with the reference's alg_state and
+    materialised intermediates (src/fesom2-accelerate.cu:256-337)."""
+    m, f = mesh("8k x 20")
+    steps = O.pre_comm_steps(m, f)
+    monkeypatch.setenv("FESOM2_NUM_KERNELS", str(k))
+    abi.set_path("stepwise")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm() == k
+        e.sync()
+        want = steps[k]
+        NT = m.N + m.H
+        if k in (1, 2):
+            assert_cols_equal(e.download("ttf_max"), want["ttf_max"], m.nlev_nod, m.L, NT, "ttf_max")
+            assert_cols_equal(e.download("ttf_min"), want["ttf_min"], m.nlev_nod, m.L, NT, "ttf_min")
+        else:
+            assert_cols_equal(e.download("ttf_max"), want["ttf_max"], m.nlev_nod, m.L, m.N, "ttf_max")
+            assert_cols_equal(e.download("ttf_min"), want["ttf_min"], m.nlev_nod, m.L, m.N, "ttf_min")
+        if k == 2:
+            assert np.array_equal(e.download("UV_rhs"), want["UV"])
+        if k >= 4:
+            assert_cols_equal(e.download("plus"), want["plus"], m.nlev_nod, m.L, m.N, "plus")
+            assert_cols_equal(e.download("minus"), want["minus"], m.nlev_nod, m.L, m.N, "minus")
+    finally:
+        e.free()
+        dm.free()
+        abi.set_path("fused")
+
+
+def test_reference_transfer_semantics():
+    """Non-resident mode keeps the reference's implicit copies: pre_comm uploads fct_LO and
+    downloads fct_plus/minus (:268, :338-339); inter_comm downloads fct_adf_v (:355); post_comm
+    uploads fct_plus/minus (:364-365) and downloads fct_adf_h (:378)."""
+    m, f = mesh("8k x 20")
+    want = O.full_pass(m, f)
+    abi.set_resident(False)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        # poison the device copy of fct_LO: pre_comm must re-upload it from the host array
+        e.upload("LO", np.full(e.host["LO"].size, 123.0))
+        assert e.pre_comm() == 6
+        e.sync()
+        assert_cols_equal(e.host["plus"], want["plus"], m.nlev_nod, m.L, m.N, "host fct_plus")
+        assert e.inter_comm() == 7
+        # the caller's exchange writes the host arrays; post_comm must upload them again
+        assert e.post_comm() == 8
+        e.sync()
+        assert np.array_equal(e.host["adf_v"], want["adf_v"])
+        assert np.array_equal(e.host["adf_h"], want["adf_h"])
+        assert e.c_step() == 9
+        e.sync()
+        assert np.array_equal(e.host["del_v"], want["del_v"])
+        assert np.array_equal(e.host["del_h"], want["del_h"])
+    finally:
+        e.free()
+        dm.free()
+        abi.set_resident(True)
+
+
+def test_invalid_mesh_fails_loudly_without_launch():
+    """An out-of-range edge node must be rejected on the host (alg_state 0), not faulted on."""
+    m, f = mesh("tiny")
+    import dataclasses
+    bad = dataclasses.replace(m, edges=m.edges.copy())
+    bad.edges[5] = m.N + 1000
+    dm = engine.DeviceMesh(bad)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm() == 0
+        assert "outside" in abi.last_error()
+    finally:
+        e.free()
+        dm.free()
+
+
+def test_repeat_is_deterministic():
+    m, f = mesh("8k x 20", perm=True)
+    _, a = run_pass(m, f)
+    _, b = run_pass(m, f)
+    for k in a:
+        assert np.array_equal(a[k].view(np.uint64), b[k].view(np.uint64)), k
+
+
+@pytest.mark.slow
+def test_full_size_1p2m_x_80():
+    """BASELINE config 2 at full size (1.2M nodes x 80 levels, full depth): exact vs the oracle."""
+    m, f = mesh("1.2M x 80", full_depth=True)
+    want = O.full_pass(m, f)
+    st, got = run_pass(m, f)
+    assert st == 9
+    check_pass(m, got, want)
