@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""FCT-ALE benchmark: full fct_ale pass (a1..c) through the C-ABI, cell-updates/s and HBM roofline.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` with one rank per GPU.  Rank 0 prints ONE JSON line.
+
+* step      one full pass of the hot path over one batch (one tracer) of synthetic input:
+            fct_ale_pre_comm_acc_ (a1..b2, fused) -> [fct_ale_exchange_acc_: RCCL halo of
+            fct_plus/fct_minus, N > 1] -> fct_ale_post_comm_c_acc_ (b3h, b3v, cv, ch).
+            Device resident: inputs are in HBM before the timed region, no host copies inside it.
+* workload  BASELINE.json configs[2]: 1.2M-node x 80-level synthetic mesh (1600 x 750 periodic
+            structured triangulation, full depth), 1 tracer, fp64 -- per GPU.  N > 1 is weak scaling:
+            the global mesh is 1600 x (750 N) split into N y-strips, each rank owning 1.2M nodes
+            (N = 8 is BASELINE configs[4]'s 9.6M-node mesh).
+* value     cell-updates/s = (sum over ranks of owned wet cells N_owned x L) / (max-over-ranks time per step).
+* roofline  the dominant kernel's algorithmic bytes per launch / its average launch time (HIP events
+            on its stream, recorded inside the library around every launch), against 8.0 TB/s.
+* cpu_baseline  the oracle's single-threaded full pass (bit-identical to reference.cpp for a1..b2)
+            on the same mesh, rank 0 at N = 1 only.
+
+Loads the engine library before torch so the process runs on one HIP runtime; torch is used only
+for the multi-rank control plane (gloo: barrier, max-reduce, RCCL unique-id broadcast).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fesom2-accelerate_amd"))
+
+import numpy as np  # noqa: E402
+
+from fesom2_amd import abi, engine, partition, synth  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
+METRIC = "FCT-ALE cell-updates/sec (nodes×levels) at 1/2/4/8 GPUs; % HBM roofline"
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------------- algorithmic bytes
+
+def mesh_stats(m):
+    """Per-pass unit counts of one local mesh (owned nodes N, L = nl-1)."""
+    ln = m.nlev_nod.astype(np.int64) - 1
+    cn = int(ln[: m.N].sum())                      # owned wet cells
+    cn_halo = int(ln[m.N:].sum())                  # halo wet cells (read by the cluster gathers)
+    ce = m.edge_cells                              # sum over edges of max(nl1, nl2)
+    # cluster sizes (unique nodes of the elements around each owned node)
+    en = m.elem2D_nodes.reshape(-1, 3) - 1
+    nie = m.nie.reshape(-1, m.dim)[: m.N] - 1
+    # unique cluster nodes per owned node (up to dim*3 candidates, -1 = padding)
+    cand = np.where(nie[:, :, None] >= 0, en[np.maximum(nie, 0)], -1).reshape(m.N, -1)
+    cand.sort(axis=1)
+    prev = np.concatenate([np.full((m.N, 1), -2), cand[:, :-1]], axis=1)
+    ring = int(((cand >= 0) & (cand != prev)).sum())
+    return dict(N=m.N, E=m.E, T=m.T, cn=cn, cn_halo=cn_halo, ce=ce, ring=ring)
+
+
+def kernel_bytes(s):
+    """Algorithmic HBM bytes per launch of each kernel of the fused pass (each array element read
+    or written once; DESIGN.md §4 derives these)."""
+    N, E, T, cn, ch, ce, ring = s["N"], s["E"], s["T"], s["cn"], s["cn_halo"], s["ce"], s["ring"]
+    cn1 = cn + N  # fct_adf_v columns carry the bottom interface too
+    ints_edges = 4 * (N + 1) + 16 * 2 * E      # node->edge CSR (EdgeRef = 16 B, two per edge)
+    p1 = 8 * (2 * (cn + ch) + cn1 + cn + ce + 2 * cn) + 4 * N + ints_edges + 4 * (N + 1) + 8 * ring + 4 * N
+    b3h = 8 * (2 * ce + 2 * (cn + ch)) + 16 * E + 4 * T
+    p2 = 8 * (2 * cn + cn1 + cn + 5 * cn + 4 * cn + ce) + 4 * N + ints_edges
+    survey = 152 * cn + 24 * ce  # SURVEY.md §8(d) B_pass without ints
+    return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "pass": p1 + b3h + p2,
+            "survey_pass": survey}
+
+
+# ----------------------------------------------------------------------------- workload
+
+def build_local(args, rank, world):
+    nx, ny, nl = synth.CONFIGS[args.config]
+    g = synth.make_mesh(nx, ny * world, nl, full_depth=not args.parity_levels,
+                        name=f"{args.config} x {world}")
+    if world == 1:
+        return g, None
+    part = partition.strip_parts(nx, ny * world, world)
+    m, halo = partition.local_mesh(g, part, rank)
+    return m, halo
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="1.2M x 80", choices=list(synth.CONFIGS))
+    ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
+    ap.add_argument("--path", default="fused", choices=["fused", "stepwise"])
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+
+    abi.dll()  # engine first: one HIP runtime for the process
+    abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    t_setup = time.perf_counter()
+    m, halo = build_local(args, rank, world)
+    f = synth.make_fields(m)
+    abi.set_resident(True)
+    abi.set_path(args.path)
+    dm = engine.DeviceMesh(m)
+    dm.prepare()
+    e = engine.FctAle(dm, f)
+    stream = e.stream
+
+    comm = plan = None
+    if world > 1:
+        import ctypes as C
+        uid = (C.c_char * 128)()
+        st = C.c_int(0)
+        if rank == 0:
+            abi.dll().fesom2_comm_unique_id_(uid, C.byref(st))
+            abi.check(st, "fesom2_comm_unique_id_")
+        t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+        dist.broadcast(t, src=0)
+        C.memmove(uid, bytes(t.numpy().tobytes()), 128)
+        comm = abi.Handle("comm")
+        abi.dll().fesom2_comm_init_(comm.ref, uid, abi.ip(rank), abi.ip(world), C.byref(st))
+        abi.check(st, "fesom2_comm_init_")
+        nb = halo.neighbors
+        sc = np.array([halo.send[q].size for q in nb], np.int32)
+        rc = np.array([halo.recv[q].size for q in nb], np.int32)
+        sn = np.ascontiguousarray(np.concatenate([halo.send[q] for q in nb]).astype(np.int32))
+        rn = np.ascontiguousarray(np.concatenate([halo.recv[q] for q in nb]).astype(np.int32))
+        ranks = np.array(nb, np.int32)
+        plan = abi.Handle("halo")
+        abi.dll().fesom2_halo_plan_(plan.ref, abi.ip(len(nb)), abi.arr(ranks), abi.arr(sc), abi.arr(sn),
+                                    abi.arr(rc), abi.arr(rn), abi.ip(m.nl), C.byref(st))
+        abi.check(st, "fesom2_halo_plan_")
+        log(f"rank {rank}: owned {m.N} halo {m.H} neighbours {nb} send {sc.tolist()} recv {rc.tolist()}")
+
+    def step():
+        s1 = e.pre_comm()
+        if s1 != 6:
+            raise RuntimeError(f"pre_comm alg_state {s1}: {abi.last_error()}")
+        if world > 1:
+            import ctypes as C
+            st = C.c_int(0)
+            abi.dll().fct_ale_exchange_acc_(C.byref(st), stream.ref, comm.ref, plan.ref, e.h["plus"].ref,
+                                            e.h["minus"].ref)
+            abi.check(st, "fct_ale_exchange_acc_")
+        if args.path == "stepwise":
+            s2 = (e.inter_comm(), e.post_comm(), e.c_step())[-1]
+        else:
+            s2 = e.post_comm_c()
+        if s2 != 9:
+            raise RuntimeError(f"phase 2 alg_state {s2}: {abi.last_error()}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    abi.device_sync()
+    setup_s = time.perf_counter() - t_setup
+
+    # ---- timed region: exactly K steps, barrier + device sync on both sides
+    abi.kernel_timing(True)
+    abi.kernel_timing_reset()
+    barrier()
+    abi.device_sync()
+    ev0, ev1 = abi.Event(), abi.Event()
+    ev0.record(stream)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    abi.device_sync()
+    t1 = time.perf_counter()
+    barrier()
+    abi.kernel_timing(False)
+    wall = t1 - t0
+    gpu_ms = ev0.elapsed_ms(ev1)
+    stats = abi.kernel_stats()
+
+    if dist is not None:
+        import torch
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+        cells = torch.tensor([mesh_stats(m)["cn"]], dtype=torch.float64)
+        dist.all_reduce(cells, op=dist.ReduceOp.SUM)
+        total_cells = float(cells.item())
+    else:
+        total_cells = float(mesh_stats(m)["cn"])
+
+    ms_step = 1e3 * wall / args.steps
+    value = total_cells / (wall / args.steps)
+
+    # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
+    s = mesh_stats(m)
+    kb = kernel_bytes(s)
+    per_kernel = {}
+    for name, (cnt, tot) in stats.items():
+        avg = tot / max(cnt, 1)
+        entry = {"launches": cnt, "avg_ms": round(avg, 4)}
+        if name in kb:
+            entry["alg_bytes"] = kb[name]
+            entry["GBps"] = round(kb[name] / (avg * 1e-3) / 1e9, 1)
+        per_kernel[name] = entry
+    dom = max(stats, key=lambda k: stats[k][1]) if stats else None
+    traffic = None
+    try:
+        with open(args.traffic) as fh:
+            tr = json.load(fh)
+        if tr.get("workload") == args.config and dom in tr.get("bytes_per_launch", {}):
+            traffic = tr["bytes_per_launch"][dom]
+    except (OSError, ValueError):
+        pass
+    roof = None
+    if dom in kb:
+        avg_s = stats[dom][1] / stats[dom][0] * 1e-3
+        achieved = kb[dom] / avg_s / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s", "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic,
+                "alg_bytes_per_launch": kb[dom], "avg_launch_ms": round(avg_s * 1e3, 4)}
+    pass_gbs = kb["survey_pass"] / (ms_step * 1e-3) / 1e9
+
+    # ---- CPU baseline (rank 0, N = 1 only)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        best, reps = O.time_full_pass(m, f, budget_s=args.cpu_budget)
+        cpu = {"value": round(s["cn"] / best, 1), "unit": "cell-updates/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
+                         f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "cell-updates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
+            "config": {"workload": f"{args.config} full-depth, 1 tracer per GPU" if not args.parity_levels
+                       else f"{args.config} parity levels, 1 tracer per GPU",
+                       "nodes_per_gpu": m.N, "levels": m.L, "global_nodes": m.N * world if world > 1 else m.N,
+                       "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
+                       "parallelism": f"node partition y-strips x{world}, RCCL halo" if world > 1 else "1 GPU",
+                       "path": args.path},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "pass_roofline": {"alg_bytes": kb["survey_pass"], "GBps": round(pass_gbs, 1),
+                              "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
+                              "note": "SURVEY.md 8(d) B_pass = 152 Cn + 24 Ce over the whole pass"},
+            "kernels": per_kernel,
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "setup_s": round(setup_s, 1),
+        }
+        print(json.dumps(out), flush=True)
+
+    e.free()
+    dm.free()
+    if world > 1:
+        abi.dll().fesom2_halo_plan_free_(plan.ref)
+        abi.dll().fesom2_comm_free_(comm.ref)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

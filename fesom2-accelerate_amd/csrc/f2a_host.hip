@@ -10,6 +10,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <atomic>
 #include <tuple>
 
 namespace f2a {
@@ -18,6 +19,7 @@ namespace {
 std::mutex g_mutex;
 int g_path = -1;
 thread_local std::string g_last_error;
+std::atomic<unsigned long> g_errors{0};
 }  // namespace
 
 int g_resident = 0;
@@ -30,6 +32,7 @@ void report(const char *fmt, ...)
     vsnprintf(msg, sizeof msg, fmt, ap);
     va_end(ap);
     g_last_error = msg;
+    g_errors++;
     fprintf(stderr, "fesom2-accelerate: %s\n", msg);
 }
 
@@ -41,6 +44,8 @@ bool ok(hipError_t st, const char *what)
 }
 
 const char *last_error() { return g_last_error.c_str(); }
+
+unsigned long error_count() { return g_errors.load(); }
 
 int kernel_path()
 {
@@ -151,6 +156,105 @@ void *DeviceArrays::alloc(size_t bytes)
     ptrs.push_back(p);
     return p;
 }
+
+// ----------------------------------------------------------------------------- kernel timing
+
+namespace {
+struct TimedLaunch {
+    std::string name;
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+bool g_timing = false;
+std::mutex g_tmutex;
+std::vector<TimedLaunch *> g_pending;
+struct Acc {
+    long count = 0;
+    double ms = 0.0;
+};
+std::map<std::string, Acc> g_acc;
+
+void resolve_pending()
+{
+    for (TimedLaunch *t : g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(t->stop) == hipSuccess && hipEventElapsedTime(&ms, t->start, t->stop) == hipSuccess) {
+            Acc &a = g_acc[t->name];
+            a.count++;
+            a.ms += ms;
+        }
+        (void)hipEventDestroy(t->start);
+        (void)hipEventDestroy(t->stop);
+        delete t;
+    }
+    g_pending.clear();
+}
+}  // namespace
+
+bool timing_enabled() { return g_timing; }
+
+void timing_begin(const char *name, hipStream_t s, void **token)
+{
+    auto *t = new TimedLaunch;
+    t->name = name;
+    if (hipEventCreate(&t->start) != hipSuccess || hipEventCreate(&t->stop) != hipSuccess) {
+        delete t;
+        *token = nullptr;
+        return;
+    }
+    (void)hipEventRecord(t->start, s);
+    *token = t;
+}
+
+void timing_end(void *token, hipStream_t s)
+{
+    auto *t = static_cast<TimedLaunch *>(token);
+    (void)hipEventRecord(t->stop, s);
+    std::lock_guard<std::mutex> lock(g_tmutex);
+    g_pending.push_back(t);
+    if (g_pending.size() > 4096) resolve_pending();
+}
+
+}  // namespace f2a
+
+extern "C" {
+
+void fesom2_kernel_timing_(int *on)
+{
+    std::lock_guard<std::mutex> lock(f2a::g_tmutex);
+    f2a::resolve_pending();
+    f2a::g_timing = on && *on;
+}
+
+void fesom2_kernel_timing_reset_(void)
+{
+    std::lock_guard<std::mutex> lock(f2a::g_tmutex);
+    f2a::resolve_pending();
+    f2a::g_acc.clear();
+}
+
+// "name count total_ms\n" lines into buf (truncated to *len bytes incl. NUL); *len = bytes needed.
+void fesom2_kernel_stats_(char *buf, int *len)
+{
+    std::lock_guard<std::mutex> lock(f2a::g_tmutex);
+    f2a::resolve_pending();
+    std::string out;
+    char line[256];
+    for (auto &kv : f2a::g_acc) {
+        snprintf(line, sizeof line, "%s %ld %.6f\n", kv.first.c_str(), kv.second.count, kv.second.ms);
+        out += line;
+    }
+    const int need = (int)out.size() + 1;
+    if (buf && *len > 0) {
+        const int n = std::min(*len - 1, (int)out.size());
+        memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    *len = need;
+}
+
+}  // extern "C"
+
+namespace f2a {
 
 // ----------------------------------------------------------------------------- plans
 

@@ -14,6 +14,7 @@ namespace f2a {
 void report(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 bool ok(hipError_t st, const char *what);
 const char *last_error();
+unsigned long error_count();  // number of report() calls so far (all threads)
 
 // ---- global modes
 extern int g_resident;  // fesom2_set_resident_
@@ -36,6 +37,22 @@ inline T *dptr(Buffer *b)
 }
 inline size_t col_bytes(long cols, int stride) { return (size_t)cols * stride * sizeof(real); }
 bool check_levels(int nl, const char *who);
+
+// ---- per-kernel timing (fesom2_kernel_timing_): HIP events recorded around each launch on the
+//      launch stream while enabled; resolved when the statistics are read.
+bool timing_enabled();
+void timing_begin(const char *name, hipStream_t s, void **token);
+void timing_end(void *token, hipStream_t s);
+// Launch through `f` with optional timing; reports failures under `name`.
+template <class F>
+bool run(const char *name, hipStream_t s, F &&f)
+{
+    void *tok = nullptr;
+    if (timing_enabled()) timing_begin(name, s, &tok);
+    const bool good = ok(f(), name);
+    if (tok) timing_end(tok, s);
+    return good;
+}
 
 // ---- device allocations owned by a plan (freed with it)
 struct DeviceArrays {

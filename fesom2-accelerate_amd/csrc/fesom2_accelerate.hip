@@ -162,7 +162,7 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         f2a::P1Args a{N, NL, *vlimit, nlev_nod, dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
                       dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
                       *dt, *flux_eps, *bignumber};
-        if (!ok(f2a::launch_p1_fused(plan->dev, a, st), "fct_ale_p1")) return;
+        if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) return;
         finish(6, {bplus, bminus});
         return;
     }
@@ -176,23 +176,22 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
     }
     const int limit = num_kernels_limit();
     real *tmax = dptr<real>(bmax), *tmin = dptr<real>(bmin);
-    if (!ok(f2a::launch_a1(NT, NL, nlev_nod, dptr<real>(blo), dptr<real>(bttf), tmax, tmin, st), "fct_ale_a1")) return;
+    if (!run("fct_ale_a1", st, [&] { return f2a::launch_a1(NT, NL, nlev_nod, dptr<real>(blo), dptr<real>(bttf), tmax, tmin, st); })) return;
     if (limit < 2) return finish(1, {bmax, bmin});
-    if (!ok(f2a::launch_a2(T, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.elem_nodes), tmax, tmin, dptr<real>(buv), *bignumber, st), "fct_ale_a2"))
+    if (!run("fct_ale_a2", st, [&] { return f2a::launch_a2(T, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.elem_nodes), tmax, tmin, dptr<real>(buv), *bignumber, st); }))
         return;
     if (limit < 3) return finish(2, {bmax, bmin, buv});
-    if (!ok(f2a::launch_a3(N, NL, *vlimit, nlev_nod, dptr<int>(mh.nie), dptr<int>(mh.nie_num), mh.dim,
-                           dptr<real>(buv), dptr<real>(blo), tmax, tmin, st), "fct_ale_a3"))
+    if (!run("fct_ale_a3", st, [&] { return f2a::launch_a3(N, NL, *vlimit, nlev_nod, dptr<int>(mh.nie), dptr<int>(mh.nie_num), mh.dim,
+                           dptr<real>(buv), dptr<real>(blo), tmax, tmin, st); }))
         return;
     if (limit < 4) return finish(3, {bmax, bmin});
-    if (!ok(f2a::launch_b1v(N, NL, nlev_nod, dptr<real>(badfv), dptr<real>(bplus), dptr<real>(bminus), st), "fct_ale_b1_vertical"))
+    if (!run("fct_ale_b1_vertical", st, [&] { return f2a::launch_b1v(N, NL, nlev_nod, dptr<real>(badfv), dptr<real>(bplus), dptr<real>(bminus), st); }))
         return;
     if (limit < 5) return finish(4, {bmax, bmin, bplus, bminus});
-    if (!ok(f2a::launch_b1h(plan->dev, NL, dptr<real>(badfh), dptr<real>(bplus), dptr<real>(bminus), st), "fct_ale_b1_horizontal"))
+    if (!run("fct_ale_b1_horizontal", st, [&] { return f2a::launch_b1h(plan->dev, NL, dptr<real>(badfh), dptr<real>(bplus), dptr<real>(bminus), st); }))
         return;
     if (limit < 6) return finish(5, {bmax, bmin, bplus, bminus});
-    if (!ok(f2a::launch_b2(N, NL, nlev_nod, dptr<real>(bainv), tmax, tmin, dptr<real>(bplus), dptr<real>(bminus), *dt, *flux_eps, st),
-            "fct_ale_b2"))
+    if (!run("fct_ale_b2", st, [&] { return f2a::launch_b2(N, NL, nlev_nod, dptr<real>(bainv), tmax, tmin, dptr<real>(bplus), dptr<real>(bminus), *dt, *flux_eps, st); }))
         return;
     finish(6, {bplus, bminus});
 }
@@ -209,7 +208,7 @@ void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **f
     Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v");
     Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
     if (!bplus || !bminus || !badfv || !bnl) return;
-    if (!ok(f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st), "fct_ale_b3_vertical"))
+    if (!run("fct_ale_b3_vertical", st, [&] { return f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st); }))
         return;
     *alg_state = 7;
     if (!g_resident && !d2h_async(badfv, st)) *alg_state = 0;
@@ -238,9 +237,8 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
     if (!plan) return;
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
-    if (!ok(f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus), dptr<real>(bminus),
-                            dptr<real>(badfh), st),
-            "fct_ale_b3_horizontal"))
+    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus), dptr<real>(bminus),
+                            dptr<real>(badfh), st); }))
         return;
     *alg_state = 8;
     if (!g_resident && !d2h_async(badfh, st)) *alg_state = 0;
@@ -270,11 +268,10 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
         return;
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
-    if (!ok(f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
-                           dptr<real>(badfv), dptr<real>(barea), dptr<real>(bdv), *dt, st),
-            "fct_ale_c_vertical"))
+    if (!run("fct_ale_c_vertical", st, [&] { return f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
+                           dptr<real>(badfv), dptr<real>(barea), dptr<real>(bdv), *dt, st); }))
         return;
-    if (!ok(f2a::launch_ch(plan->dev, NL, dptr<real>(badfh), dptr<real>(barea), dptr<real>(bdh), *dt, st), "fct_ale_c_horizontal"))
+    if (!run("fct_ale_c_horizontal", st, [&] { return f2a::launch_ch(plan->dev, NL, dptr<real>(badfh), dptr<real>(barea), dptr<real>(bdh), *dt, st); }))
         return;
     *alg_state = 9;
     if (!g_resident && (!d2h_async(bdv, st) || !d2h_async(bdh, st))) *alg_state = 0;
@@ -309,15 +306,14 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
-    if (!ok(f2a::launch_b3h(E, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.edges), dptr<int>(mh.edge_tri), dptr<real>(bplus),
-                            dptr<real>(bminus), dptr<real>(badfh), st),
-            "fct_ale_b3_horizontal"))
+    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h(E, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.edges), dptr<int>(mh.edge_tri), dptr<real>(bplus),
+                            dptr<real>(bminus), dptr<real>(badfh), st); }))
         return;
     *alg_state = 8;
     f2a::P2Args a{NL, dptr<int>(bnl), nullptr, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
                   dptr<real>(blo), dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv),
                   dptr<real>(badfh), dptr<real>(bdv), dptr<real>(bdh), *dt};
-    if (!ok(f2a::launch_p2_fused(plan->dev, a, st), "fct_ale_p2")) return;
+    if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(plan->dev, a, st); })) return;
     *alg_state = 9;
     if (!g_resident)
         for (Buffer *b : {badfv, badfh, bdv, bdh})

@@ -1,0 +1,188 @@
+// halo_rccl.hip -- device-resident halo exchange of fct_plus / fct_minus over RCCL (xGMI).
+//
+// The reference leaves `call exchange_nod(fct_plus, fct_minus)` (docs/refactoring.md:199-200,
+// :235) to the Fortran host: D2H of both arrays (src/fesom2-accelerate.cu:338-339), host MPI, and
+// H2D again (:364-365).  Here the exchange stays on the GPU: the owned columns a neighbour needs are
+// packed into one contiguous buffer, sent with grouped ncclSend/ncclRecv (point-to-point, which is
+// what xGMI links are: no ring collective), and unpacked into the halo columns, all enqueued on the
+// caller's stream.  One communicator per process/GPU (one rank per GPU).
+#include "f2a_host.hpp"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <vector>
+
+using namespace f2a;
+
+namespace {
+
+struct Comm {
+    static constexpr uint32_t kMagic = 0xF2AC0111u;
+    uint32_t magic = kMagic;
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+};
+
+struct HaloPlan {
+    static constexpr uint32_t kMagic = 0xF2A4A105u;
+    uint32_t magic = kMagic;
+    int L = 0;
+    std::vector<int> ranks, scount, rcount, soff, roff;  // offsets in columns
+    int nsend = 0, nrecv = 0, max_col = -1;
+    int *d_send = nullptr, *d_recv = nullptr;  // 0-based local columns
+    real *sbuf = nullptr, *rbuf = nullptr;     // [column][plus L | minus L]
+    DeviceArrays mem;
+};
+
+bool nccl_ok(ncclResult_t r, const char *what)
+{
+    if (r == ncclSuccess) return true;
+    report("RCCL error in %s: %s", what, ncclGetErrorString(r));
+    return false;
+}
+
+Comm *comm_of(void **h)
+{
+    if (!h || !*h || static_cast<Comm *>(*h)->magic != Comm::kMagic) {
+        report("invalid communicator handle");
+        return nullptr;
+    }
+    return static_cast<Comm *>(*h);
+}
+
+HaloPlan *plan_of(void **h)
+{
+    if (!h || !*h || static_cast<HaloPlan *>(*h)->magic != HaloPlan::kMagic) {
+        report("invalid halo plan handle");
+        return nullptr;
+    }
+    return static_cast<HaloPlan *>(*h);
+}
+
+}  // namespace
+
+extern "C" {
+
+void fesom2_comm_unique_id_(char *id128, int *istat)
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    *istat = nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId") ? 0 : 1;
+    memcpy(id128, &id, sizeof id);
+}
+
+void fesom2_comm_init_(void **comm, char *id128, int *rank, int *nranks, int *istat)
+{
+    *istat = 1;
+    auto *c = new Comm;
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof id);
+    c->rank = *rank;
+    c->nranks = *nranks;
+    if (!nccl_ok(ncclCommInitRank(&c->comm, *nranks, id, *rank), "ncclCommInitRank")) {
+        delete c;
+        *comm = nullptr;
+        return;
+    }
+    *comm = c;
+    *istat = 0;
+}
+
+void fesom2_comm_free_(void **comm)
+{
+    Comm *c = comm_of(comm);
+    if (!c) return;
+    (void)ncclCommDestroy(c->comm);
+    c->magic = 0;
+    delete c;
+    *comm = nullptr;
+}
+
+void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_counts,
+                       int *send_nodes, int *recv_counts, int *recv_nodes, int *nl, int *istat)
+{
+    *istat = 1;
+    *plan = nullptr;
+    if (*nl < 2 || *nneigh < 0) {
+        report("fesom2_halo_plan_: nl = %d, nneigh = %d", *nl, *nneigh);
+        return;
+    }
+    auto p = new HaloPlan;
+    p->L = *nl - 1;
+    std::vector<int> snodes, rnodes;
+    for (int k = 0; k < *nneigh; k++) {
+        if (send_counts[k] < 0 || recv_counts[k] < 0) {
+            report("fesom2_halo_plan_: negative count for neighbour %d", k);
+            delete p;
+            return;
+        }
+        p->ranks.push_back(neigh_ranks[k]);
+        p->scount.push_back(send_counts[k]);
+        p->rcount.push_back(recv_counts[k]);
+        p->soff.push_back(p->nsend);
+        p->roff.push_back(p->nrecv);
+        p->nsend += send_counts[k];
+        p->nrecv += recv_counts[k];
+    }
+    for (int i = 0; i < p->nsend + p->nrecv; i++) {
+        const int v = (i < p->nsend ? send_nodes[i] : recv_nodes[i - p->nsend]) - 1;
+        if (v < 0) {
+            report("fesom2_halo_plan_: node number %d < 1", v + 1);
+            delete p;
+            return;
+        }
+        (i < p->nsend ? snodes : rnodes).push_back(v);
+        p->max_col = std::max(p->max_col, v);
+    }
+    p->d_send = p->mem.upload(snodes);
+    p->d_recv = p->mem.upload(rnodes);
+    p->sbuf = static_cast<real *>(p->mem.alloc(sizeof(real) * 2 * (size_t)p->L * std::max(p->nsend, 1)));
+    p->rbuf = static_cast<real *>(p->mem.alloc(sizeof(real) * 2 * (size_t)p->L * std::max(p->nrecv, 1)));
+    if (!p->d_send || !p->d_recv || !p->sbuf || !p->rbuf) {
+        delete p;
+        return;
+    }
+    *plan = p;
+    *istat = 0;
+}
+
+void fesom2_halo_plan_free_(void **plan)
+{
+    HaloPlan *p = plan_of(plan);
+    if (!p) return;
+    p->magic = 0;
+    delete p;
+    *plan = nullptr;
+}
+
+void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void **fct_plus,
+                           void **fct_minus)
+{
+    *istat = 1;
+    Comm *c = comm_of(comm);
+    HaloPlan *p = plan_of(plan);
+    if (!c || !p) return;
+    const size_t need_bytes = col_bytes(p->max_col + 1, p->L);
+    Buffer *bp = need(fct_plus, need_bytes, "fct_plus"), *bm = need(fct_minus, need_bytes, "fct_minus");
+    if (!bp || !bm) return;
+    const hipStream_t st = stream_of(s);
+    const size_t w = 2 * (size_t)p->L;
+    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, dptr<real>(bp), dptr<real>(bm), p->sbuf, st), "halo pack"))
+        return;
+    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return;
+    for (size_t k = 0; k < p->ranks.size(); k++) {
+        if (p->scount[k] &&
+            !nccl_ok(ncclSend(p->sbuf + p->soff[k] * w, p->scount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclSend"))
+            return;
+        if (p->rcount[k] &&
+            !nccl_ok(ncclRecv(p->rbuf + p->roff[k] * w, p->rcount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclRecv"))
+            return;
+    }
+    if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd")) return;
+    if (!ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, p->rbuf, dptr<real>(bp), dptr<real>(bm), st), "halo unpack"))
+        return;
+    *istat = 0;
+}
+
+}  // extern "C"

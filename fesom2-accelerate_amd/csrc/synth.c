@@ -132,6 +132,7 @@ void synth_fill(uint64_t seed, int field, int dist, int64_t ncols, int stride, c
                 double a, double b, double *out)
 {
     const double s3 = 1.7320508075688772; /* sqrt(3) */
+#pragma omp parallel for schedule(static)
     for (int64_t c = 0; c < ncols; c++) {
         const uint64_t g = (uint64_t)(gid ? gid[c] : c) * (uint64_t)stride;
         double *o = out + c * (int64_t)stride;

@@ -24,6 +24,7 @@ EXPORTS = (
     "fesom2_prepare_mesh_", "fesom2_download_", "fesom2_upload_", "fesom2_free_", "fesom2_free_stream_",
     "fesom2_free_pinned_", "fesom2_device_sync_", "fesom2_last_error", "fesom2_event_create_",
     "fesom2_event_record_", "fesom2_event_elapsed_", "fesom2_event_free_",
+    "fesom2_kernel_timing_", "fesom2_kernel_timing_reset_", "fesom2_kernel_stats_",
     "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_halo_plan_",
     "fesom2_halo_plan_free_", "fct_ale_exchange_acc_",
 )
@@ -140,6 +141,29 @@ def device_sync():
     st = C.c_int(0)
     dll().fesom2_device_sync_(C.byref(st))
     check(st, "fesom2_device_sync_")
+
+
+def kernel_timing(on):
+    """Enable/disable per-launch HIP-event timing inside the library."""
+    dll().fesom2_kernel_timing_(ip(1 if on else 0))
+
+
+def kernel_timing_reset():
+    dll().fesom2_kernel_timing_reset_()
+
+
+def kernel_stats():
+    """{kernel name: (launches, total ms)} accumulated while timing was enabled."""
+    n = C.c_int(0)
+    dll().fesom2_kernel_stats_(None, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    n2 = C.c_int(n.value + 1)
+    dll().fesom2_kernel_stats_(buf, C.byref(n2))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms = line.split()
+        out[name] = (int(cnt), float(ms))
+    return out
 
 
 def set_mpi_rank(rank, nranks):

@@ -141,6 +141,12 @@ void fesom2_free_pinned_(void **hostptr);
 /* Device-wide synchronisation and last error string (empty if none). */
 void fesom2_device_sync_(int *istat);
 const char *fesom2_last_error(void);
+/* Per-kernel timing: while enabled, every launch is bracketed by HIP events on its stream.
+ * fesom2_kernel_stats_ writes "name count total_ms" lines (NUL-terminated, truncated to *len bytes)
+ * and sets *len to the size needed. */
+void fesom2_kernel_timing_(int *on);
+void fesom2_kernel_timing_reset_(void);
+void fesom2_kernel_stats_(char *buf, int *len);
 /* Timing: create/record/elapsed on a stream (HIP events); used by the benchmark harness. */
 void fesom2_event_create_(void **ev, int *istat);
 void fesom2_event_record_(void **ev, void **s);
