@@ -137,8 +137,8 @@ void wait_event(Buffer *b, hipStream_t s)
 
 bool check_levels(int nl, const char *who)
 {
-    if (nl < 2) {
-        report("%s: nl = %d (needs >= 2)", who, nl);
+    if (nl < 2 || nl > 1025) {
+        report("%s: nl = %d (needs 2 <= nl <= 1025)", who, nl);
         return false;
     }
     return true;
@@ -301,20 +301,33 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     }
     for (int n = 0; n < n_csr; n++) ptr[n + 1] += ptr[n];
     std::vector<EdgeRef> refs(ptr[n_csr]);
-    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
-    for (int e = 0; e < n_edges; e++) {
-        const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
-        if (n1 < n_csr) refs[pos[n1]++] = {e, n2, lev[e], 0};
-        if (n2 < n_csr) refs[pos[n2]++] = {e, n1, lev[e], 1};
+    std::vector<int> other(ptr[n_csr]);
+    {
+        std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+        for (int e = 0; e < n_edges; e++) {
+            const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
+            if (n1 < n_csr) {
+                other[pos[n1]] = n2;
+                refs[pos[n1]++] = {e, lev[e] << 1};
+            }
+            if (n2 < n_csr) {
+                other[pos[n2]] = n1;
+                refs[pos[n2]++] = {e, (lev[e] << 1) | 1};
+            }
+        }
     }
     d.edge_ptr = plan->mem.upload(ptr);
     d.edges = plan->mem.upload(refs);
     if (!d.edge_ptr || !d.edges) return fail("device allocation for the edge plan failed");
+
     // ---- clusters: the nodes of the elements around each owned node (reference.cpp:358-378
     // takes the bound over those elements' UV_rhs, which a2 built from their 3 nodes).
-    if (m.elem_nodes && m.nie && m.nie_num) {
-        std::vector<int> rptr((size_t)n_owned + 1, 0), zdry(n_owned);
-        std::vector<RingRef> ring;
+    std::vector<int> rptr, zdry;
+    std::vector<RingRef> ring;
+    const bool with_ring = m.elem_nodes && m.nie && m.nie_num;
+    if (with_ring) {
+        rptr.assign((size_t)n_owned + 1, 0);
+        zdry.assign(n_owned, 0);
         ring.reserve((size_t)n_owned * 7);
         for (int n = 0; n < n_owned; n++) {
             const int ne = m.nie_num[n];
@@ -356,12 +369,101 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         if (!d.ring_ptr || !d.ring || !d.zdry) return fail("device allocation for the cluster plan failed");
         plan->has_ring = true;
     }
+
+    // ---- processing order.  The ABI fixes the memory layout (columns in the caller's node order);
+    // the order in which the kernels VISIT nodes is free.  Greedy BFS patches of ~patch nodes
+    // (seeded at the lowest unvisited node, grown over the owned-node graph) keep the cluster and
+    // edge gathers of neighbouring columns close in time, i.e. in the XCD's L2, whatever the
+    // numbering (a row-major 1600-wide grid puts the j+-1 neighbours ~9 MB apart otherwise).
+    // Nodes inside a patch keep ascending index order.  Results do not depend on the order: each
+    // node's sums run over its own CSR in ascending edge order.
+    if (n_csr == n_owned && n_owned > 0 && m.nlev_nod) {
+        const char *env = getenv("FESOM2_PATCH");
+        const int patch = env ? atoi(env) : 64;
+        std::vector<int> order;
+        order.reserve(n_owned);
+        if (patch <= 1) {
+            for (int n = 0; n < n_owned; n++) order.push_back(n);
+        } else {
+            std::vector<char> seen(n_owned, 0);
+            std::vector<int> queue, cur;
+            int cursor = 0;
+            while ((int)order.size() < n_owned) {
+                while (seen[cursor]) cursor++;
+                queue.assign(1, cursor);
+                seen[cursor] = 1;
+                cur.clear();
+                for (size_t h = 0; h < queue.size() && (int)cur.size() < patch; h++) {
+                    const int v = queue[h];
+                    cur.push_back(v);
+                    for (int k = ptr[v]; k < ptr[v + 1]; k++) {
+                        const int w = other[k];
+                        if (w < n_owned && !seen[w]) {
+                            seen[w] = 1;
+                            queue.push_back(w);
+                        }
+                    }
+                }
+                for (size_t h = cur.size(); h < queue.size(); h++) seen[queue[h]] = 0;  // back to the pool
+                std::sort(cur.begin(), cur.end());
+                order.insert(order.end(), cur.begin(), cur.end());
+            }
+        }
+        std::vector<NodeInfo> info(n_owned);
+        std::vector<EdgeRef> pedges;
+        std::vector<RingRef> pring;
+        pedges.reserve(refs.size());
+        pring.reserve(ring.size());
+        for (int k = 0; k < n_owned; k++) {
+            const int n = order[k];
+            NodeInfo &ni = info[k];
+            ni.n = n;
+            ni.Ln = m.nlev_nod[n] - 1;
+            if (ni.Ln < 0 || ni.Ln > L) {
+                snprintf(msg, sizeof msg, "nlevels_nod2D(%d) = %d outside 1..%d", n + 1, ni.Ln + 1, nl);
+                return fail(msg);
+            }
+            ni.e0 = (int)pedges.size();
+            pedges.insert(pedges.end(), refs.begin() + ptr[n], refs.begin() + ptr[n + 1]);
+            ni.e1 = (int)pedges.size();
+            ni.r0 = (int)pring.size();
+            if (with_ring) pring.insert(pring.end(), ring.begin() + rptr[n], ring.begin() + rptr[n + 1]);
+            ni.r1 = (int)pring.size();
+            ni.zdry = with_ring ? zdry[n] : 0;
+            ni.pad = 0;
+        }
+        // edges in the order of their first visited endpoint (edges without an owned endpoint last)
+        std::vector<int4> einfo;
+        einfo.reserve(n_edges);
+        std::vector<char> etaken(n_edges, 0);
+        auto push_edge = [&](int e) {
+            etaken[e] = 1;
+            einfo.push_back(make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e));
+        };
+        for (int v : order)
+            for (int k = ptr[v]; k < ptr[v + 1]; k++)
+                if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
+        for (int e = 0; e < n_edges; e++)
+            if (!etaken[e]) push_edge(e);
+        d.node_info = plan->mem.upload(info);
+        d.p_edges = plan->mem.upload(pedges);
+        d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
+        d.p_edge_info = plan->mem.upload(einfo);
+        if (!d.node_info || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
+            return fail("device allocation for the processing order failed");
+    } else if (n_edges > 0) {
+        std::vector<int4> einfo(n_edges);
+        for (int e = 0; e < n_edges; e++)
+            einfo[e] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
+        d.p_edge_info = plan->mem.upload(einfo);
+        if (!d.p_edge_info) return fail("device allocation for the edge list failed");
+    }
     return plan;
 }
 
 namespace {
 using PlanKey = std::tuple<const void *, const void *, const void *, const void *, const void *,
-                           const void *, int, int, int, int, int>;
+                           const void *, const void *, int, int, int, int, int>;
 std::map<PlanKey, std::unique_ptr<Plan>> g_plans;
 
 template <class T>
@@ -378,7 +480,7 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
 {
     std::lock_guard<std::mutex> lock(g_mutex);
     PlanKey key{h.edges, h.edge_tri, h.nlev_elem, with_ring ? h.elem_nodes : nullptr,
-                with_ring ? h.nie : nullptr, with_ring ? h.nie_num : nullptr,
+                with_ring ? h.nie : nullptr, with_ring ? h.nie_num : nullptr, h.nlev_nod,
                 n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0};
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.get();
@@ -394,7 +496,15 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
     m.edges = edges.data();
     m.edge_tri = etri.data();
     m.nlev_elem = nle.data();
-    std::vector<int> en, nie, nnum;
+    std::vector<int> en, nie, nnum, nln;
+    if (h.nlev_nod && n_owned > 0) {
+        if (h.nlev_nod->size < sizeof(int) * (size_t)n_owned) {
+            report("nlevels_nod2D holds fewer than myDim_nod2D = %d entries", n_owned);
+            return nullptr;
+        }
+        nln = fetch<int>(h.nlev_nod, n_owned);
+        m.nlev_nod = nln.data();
+    }
     if (with_ring) {
         if (h.elem_nodes->size < 3 * sizeof(int) * (size_t)m.n_elem_total) {
             report("elem2D_nodes holds fewer than 3 x %ld entries", m.n_elem_total);
@@ -429,7 +539,7 @@ void drop_plans_of(const Buffer *b)
     for (auto it = g_plans.begin(); it != g_plans.end();) {
         const PlanKey &k = it->first;
         if (std::get<0>(k) == b || std::get<1>(k) == b || std::get<2>(k) == b || std::get<3>(k) == b ||
-            std::get<4>(k) == b || std::get<5>(k) == b)
+            std::get<4>(k) == b || std::get<5>(k) == b || std::get<6>(k) == b)
             it = g_plans.erase(it);
         else
             ++it;

@@ -71,7 +71,7 @@ struct DeviceArrays {
 
 // ---- derived mesh structures
 struct HostMesh {  // host views of the connectivity a plan is built from (nullptr = absent)
-    const int *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr;
+    const int *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr, *nlev_nod = nullptr;
     const int *elem_nodes = nullptr, *nie = nullptr, *nie_num = nullptr;
     long n_elem_total = 0;
     int dim = 0;
@@ -90,7 +90,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                                  int n_csr, int nl, std::string &err);
 
 struct MeshHandles {
-    Buffer *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr;
+    Buffer *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr, *nlev_nod = nullptr;
     Buffer *elem_nodes = nullptr, *nie = nullptr, *nie_num = nullptr;
     int dim = 0;
 };

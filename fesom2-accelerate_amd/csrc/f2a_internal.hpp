@@ -26,10 +26,9 @@ struct Buffer {
 // One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the
 // order in which the reference's edge loops touch the node: reference.cpp:406-425).
 struct EdgeRef {
-    int edge;   // 0-based local edge
-    int other;  // 0-based other endpoint
-    int lev;    // max(nl1, nl2) = levels the edge carries (reference.cpp:412-414)
-    int flags;  // bit0: this node is edges(2,e) (second endpoint); bit1: this node writes fct_adf_h(:,e)
+    int edge;  // 0-based local edge
+    int code;  // (lev << 1) | second: lev = max(nl1, nl2) levels the edge carries
+               // (reference.cpp:412-414); second = this node is edges(2,e)
 };
 
 // One node of a node's cluster (the union of the nodes of its adjacent elements).  `lev` is the
@@ -38,6 +37,17 @@ struct EdgeRef {
 struct RingRef {
     int node;
     int lev;
+};
+
+// One owned node at one position of the processing order (32 bytes, one load per cell).
+// [r0, r1) / [e0, e1) index the processing-order copies of the cluster / edge CSRs.
+struct NodeInfo {
+    int n;     // 0-based local node
+    int Ln;    // nlevels_nod2D(n) - 1
+    int r0, r1;
+    int e0, e1;
+    int zdry;  // min over adjacent elements of (nlevels(e) - 1); levels >= zdry see the a2 fill
+    int pad;
 };
 
 // Device-side view of the derived mesh structures of one (mesh, partition) pair.
@@ -53,6 +63,13 @@ struct MeshPlanDev {
     const int *ring_ptr = nullptr;     // [n_owned + 1]
     const RingRef *ring = nullptr;
     const int *zdry = nullptr;         // [n_owned] min over adjacent elements of (nlevels(e)-1)
+    // locality-aware processing order (compact BFS patches of the node graph, see build_plan):
+    // owned nodes and local edges in the order the fused kernels visit them, with the CSRs
+    // re-laid out in that order
+    const NodeInfo *node_info = nullptr;  // [n_owned]
+    const EdgeRef *p_edges = nullptr;     // node->edge CSR, processing order
+    const RingRef *p_ring = nullptr;      // cluster CSR, processing order (if has ring)
+    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order
     // local edges with no owned endpoint (b3-horizontal still applies to them)
     const int *orphan_edges = nullptr;
     int n_orphans = 0;
@@ -70,14 +87,18 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 
 struct P2Args {
     int nl;
-    const int *nlev_nod;
-    const int *nodes;   // node list to process (nullptr = 0..count-1)
+    const NodeInfo *nodes;  // processing positions to run (a subset of the plan's node_info)
     int count;
     const real *plus, *minus, *ttf, *LO, *hnode, *hnode_new, *area;
     real *adf_v, *adf_h, *del_v, *del_h;
     real dt;
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
+// b3-horizontal over all local edges of the plan (edge groups, flat levels)
+hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
+                            real *adf_h, hipStream_t s);
+// columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
+int group_columns(int L);
 
 // Stepwise kernels, one per reference step.
 hipError_t launch_a1(int n_nodes, int nl, const int *nlev_nod, const real *LO, const real *ttf,

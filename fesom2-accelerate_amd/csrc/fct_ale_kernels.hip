@@ -15,12 +15,14 @@
 // reproducible.  max/min are written as std::max/std::min ternaries, and the library is compiled
 // with -ffp-contract=off so no multiply-add is fused (the x86-64 reference has none).
 //
-// Mapping: one wave64 per node column (or element / edge), lanes over vertical levels, 4 waves per
-// 256-thread workgroup, and an XCD-aware block swizzle so each XCD's L2 walks a contiguous range
-// of the (spatially sorted) mesh: neighbouring columns gathered by the cluster/edge loops are then
-// L2/Infinity-Cache hits rather than HBM re-reads.
+// Mapping: stepwise kernels use one wave64 per node column (or element / edge) with lanes over
+// levels; the fused kernels give each wave a group of whole columns flattened over its lanes (see
+// "fused kernels").  4 waves per 256-thread workgroup, and an XCD-aware block swizzle so each XCD's
+// L2 walks a contiguous range of the (spatially sorted) mesh: neighbouring columns gathered by the
+// cluster/edge loops are then L2/Infinity-Cache hits rather than HBM re-reads.
 #include "f2a_internal.hpp"
 #include <cmath>
+#include <cstdlib>
 
 namespace f2a {
 
@@ -33,10 +35,25 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 
 // Bijective XCD-aware swizzle: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // residue class a contiguous range of tiles.  Speed only, never correctness.
+__constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements)
+
 __device__ __forceinline__ int xcd_tile(int b, int G)
 {
+    if (!c_xcd_swizzle) return b;
     const int q = G >> 3, r = G & 7, x = b & 7, k = b >> 3;
     return x * q + (x < r ? x : r) + k;
+}
+
+static void init_swizzle()
+{
+    static bool done = false;
+    if (done) return;
+    done = true;
+    const char *e = getenv("FESOM2_XCD");
+    if (e && atoi(e) == 0) {
+        const int zero = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_xcd_swizzle), &zero, sizeof zero);
+    }
 }
 
 __device__ __forceinline__ int wave_item()
@@ -196,15 +213,15 @@ __global__ __launch_bounds__(kBlock) void k_b1h(MeshPlanDev mp, int L, const rea
     const int lane = threadIdx.x & 63;
     const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
     int lmax = 0;
-    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].lev);
+    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].code >> 1);
     const size_t b = (size_t)n * L;
     for (int z = lane; z < lmax; z += kWave) {
         real p = plus[b + z], m = minus[b + z];
         for (int k = e0; k < e1; k++) {
             const EdgeRef er = mp.edges[k];
-            if (z < er.lev) {
+            if (z < (er.code >> 1)) {
                 const real h = adf_h[(size_t)er.edge * L + z];
-                if (er.flags & 1) {
+                if (er.code & 1) {
                     p += RMAX(0., -h);
                     m += RMIN(0., -h);
                 } else {
@@ -350,16 +367,16 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
     const int lane = threadIdx.x & 63;
     const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
     int lmax = 0;
-    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].lev);
+    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].code >> 1);
     const size_t b = (size_t)n * L, a = (size_t)n * (L + 1);
     for (int z = lane; z < lmax; z += kWave) {
         const real dta = dt / area[a + z];
         real d = del_h[b + z];
         for (int k = e0; k < e1; k++) {
             const EdgeRef er = mp.edges[k];
-            if (z < er.lev) {
+            if (z < (er.code >> 1)) {
                 const real h = adf_h[(size_t)er.edge * L + z];
-                d = (er.flags & 1) ? d - h * dta : d + h * dta;
+                d = (er.code & 1) ? d - h * dta : d + h * dta;
             }
         }
         del_h[b + z] = d;
@@ -367,141 +384,256 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 }
 
 // ============================================================================ fused kernels
+//
+// One thread per cell.  A block owns G whole columns (node columns for phases 1/2, edge columns for
+// b3h) taken in the plan's processing order: thread t is cell (j, z) = (t / L, t % L), and the block
+// has G*L threads rounded up to the wave size (L = 80, G = 4: 320 threads, 5 full waves).  A column
+// group therefore completes within one chain of memory latencies, and the XCD's in-flight window
+// stays a few hundred columns wide, which is what lets neighbouring columns' gathers hit its L2.
+// Columns never straddle blocks, so the LDS stencil of phase 1 and the in-place fct_adf_v update of
+// phase 2 only need block barriers.  Cluster / edge lists are read in batches of kBatch so all of a
+// thread's gathers are in flight together.
 
-// Phase 1: a1 + a2 + a3 + b1v + b1h + b2 for one owned node per wave.
-// The cluster bound tvert(z) = max over adjacent elements e of UV_rhs(e, z) is computed straight
-// from ttf/LO over the node's cluster (RingRef list): a cluster node k contributes on levels
-// z < ring.lev (the element-level mask of a2), and the a2 fill -bignumber enters wherever some
-// adjacent element is dry (z >= zdry).  max/min are exact, so regrouping them leaves the values of
-// reference.cpp:321-378 unchanged.  The vertical 3-point stencil reads tvert from LDS.
+static constexpr int kBatch = 8;
+
+// t -> (column j, level z) for t < G*L, exact: the float quotient stays far from an integer
+__device__ __forceinline__ void cell_of(int t, int L, float invL, int &j, int &z)
+{
+    j = (int)(((float)t + 0.5f) * invL);
+    z = t - j * L;
+}
+
+__device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
+
+// tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
+// straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
+__device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
+                                              const real *__restrict__ LO,
+                                              const real *__restrict__ ttf, int z, int L, bool dry,
+                                              real big, real &vx, real &vn)
+{
+    vx = dry ? -big : -INFINITY;
+    vn = dry ? big : INFINITY;
+    for (int r = r0; r < r1; r += kBatch) {
+        size_t idx[kBatch];
+        bool on[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const RingRef rr = (r + k < r1) ? ring[r + k] : RingRef{0, 0};
+            idx[k] = (size_t)rr.node * L + z;
+            on[k] = z < rr.lev;
+        }
+        real lo[kBatch], tt[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            lo[k] = on[k] ? LO[idx[k]] : 0.;
+            tt[k] = on[k] ? ttf[idx[k]] : 0.;
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+            if (on[k]) {
+                vx = RMAX(vx, RMAX(lo[k], tt[k]));
+                vn = RMIN(vn, RMIN(lo[k], tt[k]));
+            }
+    }
+}
+
+// Antidiffusive edge sums of one node level in ascending edge order (reference.cpp:406-425).
+__device__ __forceinline__ void edge_sums(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                          const real *__restrict__ adf_h, int z, int L, real &p,
+                                          real &m)
+{
+    for (int k0 = e0; k0 < e1; k0 += kBatch) {
+        size_t idx[kBatch];
+        int code[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const EdgeRef er = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0};
+            idx[k] = (size_t)er.edge * L + z;
+            code[k] = er.code;
+        }
+        real h[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) h[k] = (z < (code[k] >> 1)) ? adf_h[idx[k]] : 0.;
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+            if (z < (code[k] >> 1)) {
+                if (code[k] & 1) {
+                    p += RMAX(0., -h[k]);
+                    m += RMIN(0., -h[k]);
+                } else {
+                    p += RMAX(0., h[k]);
+                    m += RMIN(0., h[k]);
+                }
+            }
+    }
+}
+
+// Phase 1: a1 + a2 + a3 + b1v + b1h + b2 for G node columns per block.  Before the barrier every
+// thread issues all of its loads (cluster gathers for tvert, edge gathers for b1h, its own column);
+// after it the vertical 3-point stencil of tvert is read from LDS and the limiter ratios stored.
 template <int VLIMIT>
-__global__ __launch_bounds__(kBlock) void k_p1(MeshPlanDev mp, P1Args a)
+__global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invL)
 {
     extern __shared__ real lds[];
-    const int n = wave_item();
-    if (n >= a.n_owned) return;
-    const int lane = threadIdx.x & 63;
     const int L = a.nl - 1;
-    real *tvx = lds + (threadIdx.x >> 6) * 2 * L;
-    real *tvn = tvx + L;
-    const int Ln = a.nlev_nod[n] - 1;
-    const int r0 = mp.ring_ptr[n], r1 = mp.ring_ptr[n + 1];
-    const int zd = mp.zdry[n];
-    for (int z = lane; z < Ln; z += kWave) {
-        real vx = (z >= zd) ? -a.big : -INFINITY;
-        real vn = (z >= zd) ? a.big : INFINITY;
-        for (int r = r0; r < r1; r++) {
-            const RingRef rr = mp.ring[r];
-            if (z < rr.lev) {
-                const size_t i = (size_t)rr.node * L + z;
-                const real lo = a.LO[i], t = a.ttf[i];
-                vx = RMAX(vx, RMAX(lo, t));
-                vn = RMIN(vn, RMIN(lo, t));
-            }
-        }
-        tvx[z] = vx;
-        tvn[z] = vn;
+    const int t = threadIdx.x;
+    int j, z;
+    cell_of(t, L, invL, j, z);
+    const int k = block_tile() * G + j;
+    const bool col = j < G && k < a.n_owned;
+    NodeInfo ni{};
+    if (col) ni = mp.node_info[k];
+    const bool wet = col && z < ni.Ln;
+    real vx = 0., vn = 0., p = 0., m = 0., lo = 0., ai = 0.;
+    size_t b = 0;
+    if (wet) {
+        b = (size_t)ni.n * L + z;
+        const size_t ab = (size_t)ni.n * a.nl + z;
+        lo = a.LO[b];
+        ai = a.area_inv[ab];
+        const real v0 = a.adf_v[ab], v1 = a.adf_v[ab + 1];
+        cluster_bound(mp.p_ring, ni.r0, ni.r1, a.LO, a.ttf, z, L, z >= ni.zdry, a.big, vx, vn);
+        p = RMAX(0., v0) + RMAX(0., -v1);
+        m = RMIN(0., v0) + RMIN(0., -v1);
+        edge_sums(mp.p_edges, ni.e0, ni.e1, a.adf_h, z, L, p, m);
     }
-    wave_lds_sync();
-    const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
-    const size_t b = (size_t)n * L, ab = (size_t)n * a.nl;
-    for (int z = lane; z < Ln; z += kWave) {
-        const real lo = a.LO[b + z];
-        real tm, tn;
-        if (VLIMIT == 1) {
-            if (z == 0 || z == Ln - 1) {
-                tm = tvx[z];
-                tn = tvn[z];
-            } else {
-                tm = RMAX(RMAX(tvx[z - 1], tvx[z]), tvx[z + 1]);
-                tn = RMIN(RMIN(tvn[z - 1], tvn[z]), tvn[z + 1]);
-            }
+    real *tvx = lds, *tvn = lds + G * L;
+    if (t < G * L) {
+        tvx[t] = vx;
+        tvn[t] = vn;
+    }
+    __syncthreads();
+    if (!wet) return;
+    const int Ln = ni.Ln;
+    real tm, tn;
+    if (VLIMIT == 1) {
+        if (z == 0 || z == Ln - 1) {
+            tm = tvx[t];
+            tn = tvn[t];
         } else {
-            tm = tvx[z];
-            tn = tvn[z];
-            if (z >= 1 && z < Ln - 1) {
-                const real c0 = RMAX(a.LO[b + z - 1], a.ttf[b + z - 1]);
-                const real c1 = RMAX(lo, a.ttf[b + z]);
-                const real c2 = RMAX(a.LO[b + z + 1], a.ttf[b + z + 1]);
-                const real hmx = RMAX(RMAX(c0, c1), c2);
-                const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
-                if (VLIMIT == 2) {
-                    tm = RMAX(tm, hmx);
-                    tn = RMIN(tn, hmn);
-                } else {
-                    tm = RMIN(tm, hmx);
-                    tn = RMAX(tn, hmn);
-                }
+            tm = RMAX(RMAX(tvx[t - 1], tvx[t]), tvx[t + 1]);
+            tn = RMIN(RMIN(tvn[t - 1], tvn[t]), tvn[t + 1]);
+        }
+    } else {
+        tm = tvx[t];
+        tn = tvn[t];
+        if (z >= 1 && z < Ln - 1) {
+            const real c0 = RMAX(a.LO[b - 1], a.ttf[b - 1]);
+            const real c1 = RMAX(lo, a.ttf[b]);
+            const real c2 = RMAX(a.LO[b + 1], a.ttf[b + 1]);
+            const real hmx = RMAX(RMAX(c0, c1), c2);
+            const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
+            if (VLIMIT == 2) {
+                tm = RMAX(tm, hmx);
+                tn = RMIN(tn, hmn);
+            } else {
+                tm = RMIN(tm, hmx);
+                tn = RMAX(tn, hmn);
             }
         }
-        const real fmx = tm - lo, fmn = tn - lo;
-        const real v0 = a.adf_v[ab + z], v1 = a.adf_v[ab + z + 1];
-        real p = RMAX(0., v0) + RMAX(0., -v1);
-        real m = RMIN(0., v0) + RMIN(0., -v1);
-        for (int k = e0; k < e1; k++) {
-            const EdgeRef er = mp.edges[k];
-            if (z < er.lev) {
-                const real h = a.adf_h[(size_t)er.edge * L + z];
-                if (er.flags & 1) {
-                    p += RMAX(0., -h);
-                    m += RMIN(0., -h);
-                } else {
-                    p += RMAX(0., h);
-                    m += RMIN(0., h);
-                }
-            }
-        }
-        const real ai = a.area_inv[ab + z];
-        real flux = p * a.dt * ai + a.eps;
-        a.plus[b + z] = RMIN(1., fmx / flux);
-        flux = m * a.dt * ai - a.eps;
-        a.minus[b + z] = RMIN(1., fmn / flux);
     }
+    real flux = p * a.dt * ai + a.eps;  // reference.cpp:432-435
+    a.plus[b] = RMIN(1., (tm - lo) / flux);
+    flux = m * a.dt * ai - a.eps;
+    a.minus[b] = RMIN(1., (tn - lo) / flux);
 }
 
-// Phase 2 node part: b3v + cv + ch for one owned node per wave.  fct_adf_h must already hold the
-// b3-limited fluxes (k_b3h runs first, as in docs/refactoring.md:237-314).  The limited vertical
-// flux of interface z+1 is recomputed in-lane from plus/minus(z, z+1) (bottom interface nlev-1 is
-// never limited), so the column is read once and written once.
-__global__ __launch_bounds__(kBlock) void k_p2(MeshPlanDev mp, P2Args a)
+// Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
+__global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, int n_edges, int L,
+                                                int G, float invL, const real *__restrict__ plus,
+                                                const real *__restrict__ minus,
+                                                real *__restrict__ adf_h)
 {
-    int i = wave_item();
-    if (i >= a.count) return;
-    const int n = a.nodes ? __builtin_amdgcn_readfirstlane(a.nodes[i]) : i;
-    const int lane = threadIdx.x & 63;
+    int j, z;
+    cell_of(threadIdx.x, L, invL, j, z);
+    const int k = block_tile() * G + j;
+    if (j >= G || k >= n_edges) return;
+    const int4 ei = einfo[k];  // {node1, node2, lev, edge}
+    if (z >= ei.z) return;
+    const size_t i = (size_t)ei.w * L + z;
+    const size_t i1 = (size_t)ei.x * L + z, i2 = (size_t)ei.y * L + z;
+    const real f = adf_h[i];
+    adf_h[i] = b3h_factor(f, plus[i1], minus[i1], plus[i2], minus[i2]) * f;
+}
+
+// Phase 2, nodes: b3v + cv + ch, G node columns per block.  fct_adf_h already holds the b3-limited
+// fluxes (k_b3h_g ran first, as in docs/refactoring.md:237-314).  The limited vertical flux of
+// interface z+1 is recomputed in-thread from plus/minus(z, z+1) (the bottom interface nlev-1 is
+// never limited); the barrier orders every raw fct_adf_v read of the block before its writes.
+__global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invL)
+{
     const int L = a.nl - 1;
-    const int Ln = a.nlev_nod[n] - 1;
-    const size_t b = (size_t)n * L, ab = (size_t)n * a.nl;
-    const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
-    const int top = Ln > 1 ? Ln : 1;
-    for (int z = lane; z < top; z += kWave) {
-        const real pz = a.plus[b + z], mz = a.minus[b + z];
-        const real pm = z ? a.plus[b + z - 1] : 0., mm = z ? a.minus[b + z - 1] : 0.;
-        const real f0 = a.adf_v[ab + z], f1 = a.adf_v[ab + z + 1];
-        const real l0 = b3v_factor(z, f0, pm, mm, pz, mz) * f0;
-        real l1 = f1;
-        if (z + 1 < Ln) l1 = b3v_factor(z + 1, f1, pz, mz, a.plus[b + z + 1], a.minus[b + z + 1]) * f1;
-        a.adf_v[ab + z] = l0;
-        if (z >= Ln) continue;  // Ln == 0: only the Fortran's nz = 1 limiting applies
-        const real ar = a.area[ab + z];
-        const real dta = a.dt / ar;
-        real t = a.del_v[b + z] - a.ttf[b + z] * a.hnode[b + z];
-        t = t + a.LO[b + z] * a.hnode_new[b + z];
-        t = t + (l0 - l1) * dta;
-        a.del_v[b + z] = t;
-        real d = a.del_h[b + z];
-        for (int k = e0; k < e1; k++) {
-            const EdgeRef er = mp.edges[k];
-            if (z < er.lev) {
-                const real h = a.adf_h[(size_t)er.edge * L + z];
-                d = (er.flags & 1) ? d - h * dta : d + h * dta;
+    const int t = threadIdx.x;
+    int j, z;
+    cell_of(t, L, invL, j, z);
+    const int k = block_tile() * G + j;
+    const bool col = j < G && k < a.count;
+    NodeInfo ni{};
+    if (col) ni = a.nodes[k];
+    const int Ln = ni.Ln;
+    const bool act = col && z < (Ln > 1 ? Ln : 1);  // the Fortran always limits nz = 1
+    const bool wet = col && z < Ln;
+    real l0 = 0., dv = 0., dh = 0.;
+    size_t b = 0, ab = 0;
+    if (act) {
+        b = (size_t)ni.n * L + z;
+        ab = (size_t)ni.n * a.nl + z;
+        const real pz = a.plus[b], mz = a.minus[b];
+        const real pm = z ? a.plus[b - 1] : 0., mm = z ? a.minus[b - 1] : 0.;
+        const bool below = z + 1 < Ln;
+        const real pz1 = below ? a.plus[b + 1] : 0., mz1 = below ? a.minus[b + 1] : 0.;
+        const real f0 = a.adf_v[ab], f1 = a.adf_v[ab + 1];
+        l0 = b3v_factor(z, f0, pm, mm, pz, mz) * f0;
+        if (wet) {
+            const real l1 = below ? b3v_factor(z + 1, f1, pz, mz, pz1, mz1) * f1 : f1;
+            const real dta = a.dt / a.area[ab];
+            dv = a.del_v[b] - a.ttf[b] * a.hnode[b];
+            dv = dv + a.LO[b] * a.hnode_new[b];
+            dv = dv + (l0 - l1) * dta;
+            dh = a.del_h[b];
+            for (int k0 = ni.e0; k0 < ni.e1; k0 += kBatch) {
+                size_t idx[kBatch];
+                int code[kBatch];
+#pragma unroll
+                for (int q = 0; q < kBatch; q++) {
+                    const EdgeRef er = (k0 + q < ni.e1) ? mp.p_edges[k0 + q] : EdgeRef{0, 0};
+                    idx[q] = (size_t)er.edge * L + z;
+                    code[q] = er.code;
+                }
+                real h[kBatch];
+#pragma unroll
+                for (int q = 0; q < kBatch; q++) h[q] = (z < (code[q] >> 1)) ? a.adf_h[idx[q]] : 0.;
+#pragma unroll
+                for (int q = 0; q < kBatch; q++)  // ascending edge order (docs/refactoring.md:303-314)
+                    if (z < (code[q] >> 1)) dh = (code[q] & 1) ? dh - h[q] * dta : dh + h[q] * dta;
             }
         }
-        a.del_h[b + z] = d;
     }
-    // levels the node's edges carry beyond its own column never occur on a consistent mesh
-    // (nlevels_nod2D = max over adjacent elements), so no second loop is needed.
+    __syncthreads();
+    if (!act) return;
+    a.adf_v[ab] = l0;
+    if (!wet) return;
+    a.del_v[b] = dv;
+    a.del_h[b] = dh;
 }
+
+int group_columns(int L)
+{
+    int best = 1;
+    double best_waste = 1e30;
+    for (int G = 1; G * L <= 1024; G *= 2) {
+        const double waste = (double)(((G * L + kWave - 1) / kWave) * kWave) / (G * L);
+        if (waste < best_waste - 1e-9) {
+            best_waste = waste;
+            best = G;
+        }
+        if (waste < 1.0 + 1e-9) break;
+    }
+    return best;
+}
+
+static inline unsigned threads_for(int G, int L) { return (unsigned)(((G * L + kWave - 1) / kWave) * kWave); }
 
 // ============================================================================ halo pack / unpack
 
@@ -537,6 +669,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack(const int *__restrict__ nodes
 
 #define F2A_LAUNCH(kernel, items, lds_bytes, s, ...)                                    \
     do {                                                                                \
+        init_swizzle();                                                                 \
         if ((items) > 0)                                                                \
             hipLaunchKernelGGL(kernel, dim3(grid_for(items)), dim3(kBlock), (lds_bytes), \
                                (s), __VA_ARGS__);                                       \
@@ -621,17 +754,41 @@ hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const rea
     F2A_LAUNCH(k_ch, mp.n_owned, 0, s, mp, nl - 1, adf_h, area, del_h, dt);
 }
 
+// L <= 1024 levels (one block per column at most); checked by the host entry points.
+#define F2A_LAUNCH_GROUPS(kernel, groups, G, L, lds_bytes, s, ...)                                       \
+    do {                                                                                                \
+        init_swizzle();                                                                                 \
+        if ((groups) > 0)                                                                               \
+            hipLaunchKernelGGL(kernel, dim3((unsigned)(groups)), dim3(threads_for(G, L)), (lds_bytes), \
+                               (s), __VA_ARGS__);                                                       \
+        return hipGetLastError();                                                                       \
+    } while (0)
+
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
-    const size_t lds = (size_t)kWavesPerBlock * 2 * (a.nl - 1) * sizeof(real);
-    if (a.vlimit == 2) F2A_LAUNCH(k_p1<2>, a.n_owned, lds, s, mp, a);
-    if (a.vlimit == 3) F2A_LAUNCH(k_p1<3>, a.n_owned, lds, s, mp, a);
-    F2A_LAUNCH(k_p1<1>, a.n_owned, lds, s, mp, a);
+    const int L = a.nl - 1, G = group_columns(L);
+    const float invL = 1.0f / (float)L;
+    const long groups = (a.n_owned + G - 1) / G;
+    const size_t lds = 2 * (size_t)G * L * sizeof(real);
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS(k_p1<2>, groups, G, L, lds, s, mp, a, G, invL);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS(k_p1<3>, groups, G, L, lds, s, mp, a, G, invL);
+    F2A_LAUNCH_GROUPS(k_p1<1>, groups, G, L, lds, s, mp, a, G, invL);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
-    F2A_LAUNCH(k_p2, a.count, 0, s, mp, a);
+    const int L = a.nl - 1, G = group_columns(L);
+    const long groups = (a.count + G - 1) / G;
+    F2A_LAUNCH_GROUPS(k_p2, groups, G, L, 0, s, mp, a, G, 1.0f / (float)L);
+}
+
+hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
+                            real *adf_h, hipStream_t s)
+{
+    const int L = nl - 1, G = group_columns(L);
+    const long groups = (mp.n_edges + G - 1) / G;
+    F2A_LAUNCH_GROUPS(k_b3h_g, groups, G, L, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)L, plus, minus,
+                      adf_h);
 }
 
 hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,

@@ -139,6 +139,7 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         !buv || !bainv)
         return;
     const bool stepwise = kernel_path() == 1;
+    mh.nlev_nod = bnlnod;
     const Plan *plan = get_plan(mh, N, NT, E, NL, !stepwise);
     if (!plan) return;
 
@@ -266,6 +267,7 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
     mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
     if (!bdv || !bdh || !bttf || !blo || !bh || !bhn || !badfv || !badfh || !barea || !bnl || !mh.edges || !mh.edge_tri || !mh.nlev_elem)
         return;
+    mh.nlev_nod = bnl;
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     if (!run("fct_ale_c_vertical", st, [&] { return f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
@@ -303,14 +305,14 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
     if (!bplus || !bminus || !bdv || !bdh || !bttf || !blo || !bh || !bhn || !badfv || !badfh || !barea || !bnl ||
         !mh.edges || !mh.edge_tri || !mh.nlev_elem)
         return;
+    mh.nlev_nod = bnl;
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
-    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h(E, NL, dptr<int>(mh.nlev_elem), dptr<int>(mh.edges), dptr<int>(mh.edge_tri), dptr<real>(bplus),
-                            dptr<real>(bminus), dptr<real>(badfh), st); }))
+    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h_fused(plan->dev, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), st); }))
         return;
     *alg_state = 8;
-    f2a::P2Args a{NL, dptr<int>(bnl), nullptr, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
+    f2a::P2Args a{NL, plan->dev.node_info, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
                   dptr<real>(blo), dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv),
                   dptr<real>(badfh), dptr<real>(bdv), dptr<real>(bdh), *dt};
     if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(plan->dev, a, st); })) return;
@@ -346,6 +348,7 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
     mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
     mh.dim = *nod_in_elem2D_dim;
     if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
+    mh.nlev_nod = bnlnod;
     if (get_plan(mh, N, NT, E, *nl, true) && get_plan(mh, N, NT, E, *nl, false)) *istat = 0;
 }
 
