@@ -385,63 +385,104 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 
 // ============================================================================ fused kernels
 //
-// One thread per cell.  A block owns G whole columns (node columns for phases 1/2, edge columns for
-// b3h) taken in the plan's processing order: thread t is cell (j, z) = (t / L, t % L), and the block
-// has G*L threads rounded up to the wave size (L = 80, G = 4: 320 threads, 5 full waves).  A column
-// group therefore completes within one chain of memory latencies, and the XCD's in-flight window
-// stays a few hundred columns wide, which is what lets neighbouring columns' gathers hit its L2.
-// Columns never straddle blocks, so the LDS stencil of phase 1 and the in-place fct_adf_v update of
-// phase 2 only need block barriers.  Cluster / edge lists are read in batches of kBatch so all of a
-// thread's gathers are in flight together.
+// C levels per thread (C = 2 when L is even: ttf/LO/adf_h/plus/minus/del_* are then read and written
+// as 16-byte pairs; arrays of stride nl = L+1 -- fct_adf_v, area, area_inv -- stay 8-byte because
+// their columns alternate 16-byte alignment).  A block owns G whole columns (node columns for phases
+// 1/2, edge columns for b3h) taken in the plan's processing order; thread t is the level pair
+// z0 = C*(t % (L/C)) of column t / (L/C), and the block has G*L/C threads rounded up to the wave
+// size (L = 80, C = 2, G = 8: 320 threads, 5 full waves).  A column group completes within one chain
+// of memory latencies and the XCD's in-flight window stays a few hundred columns wide, which is
+// what lets neighbouring columns' gathers hit its L2.  Columns never straddle blocks, so the LDS
+// stencil of phase 1 and the in-place fct_adf_v update of phase 2 only need block barriers.
 
 static constexpr int kBatch = 8;
 
-// t -> (column j, level z) for t < G*L, exact: the float quotient stays far from an integer
-__device__ __forceinline__ void cell_of(int t, int L, float invL, int &j, int &z)
+// t -> (column j, slot u) for t < G*S (S slots per column), exact: the float quotient stays far
+// from an integer
+__device__ __forceinline__ void slot_of(int t, int S, float invS, int &j, int &u)
 {
-    j = (int)(((float)t + 0.5f) * invL);
-    z = t - j * L;
+    j = (int)(((float)t + 0.5f) * invS);
+    u = t - j * S;
 }
 
 __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
 
-// tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
-// straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
-__device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
-                                              const real *__restrict__ LO,
-                                              const real *__restrict__ ttf, int z, int L, bool dry,
-                                              real big, real &vx, real &vn)
+template <int C>
+__device__ __forceinline__ void ldv(const real *__restrict__ p, real (&v)[C])
 {
-    vx = dry ? -big : -INFINITY;
-    vn = dry ? big : INFINITY;
-    for (int r = r0; r < r1; r += kBatch) {
-        size_t idx[kBatch];
-        bool on[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            const RingRef rr = (r + k < r1) ? ring[r + k] : RingRef{0, 0};
-            idx[k] = (size_t)rr.node * L + z;
-            on[k] = z < rr.lev;
-        }
-        real lo[kBatch], tt[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            lo[k] = on[k] ? LO[idx[k]] : 0.;
-            tt[k] = on[k] ? ttf[idx[k]] : 0.;
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; k++)
-            if (on[k]) {
-                vx = RMAX(vx, RMAX(lo[k], tt[k]));
-                vn = RMIN(vn, RMIN(lo[k], tt[k]));
-            }
+    if constexpr (C == 1) {
+        v[0] = p[0];
+    } else {
+        const double2 t = *reinterpret_cast<const double2 *>(p);
+        v[0] = t.x;
+        v[1] = t.y;
     }
 }
 
-// Antidiffusive edge sums of one node level in ascending edge order (reference.cpp:406-425).
-__device__ __forceinline__ void edge_sums(const EdgeRef *__restrict__ edges, int e0, int e1,
-                                          const real *__restrict__ adf_h, int z, int L, real &p,
-                                          real &m)
+// store the first `n` (1..C) values
+template <int C>
+__device__ __forceinline__ void stv(real *__restrict__ p, const real (&v)[C], int n)
+{
+    if constexpr (C == 1) {
+        p[0] = v[0];
+    } else {
+        if (n == 2)
+            *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
+        else
+            p[0] = v[0];
+    }
+}
+
+// tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
+// straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
+template <int C>
+__device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
+                                              const real *__restrict__ LO,
+                                              const real *__restrict__ ttf, int z0, int L, int zdry,
+                                              real big, real (&vx)[C], real (&vn)[C])
+{
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        const bool dry = z0 + c >= zdry;
+        vx[c] = dry ? -big : -INFINITY;
+        vn[c] = dry ? big : INFINITY;
+    }
+    for (int r = r0; r < r1; r += kBatch) {
+        size_t idx[kBatch];
+        int lev[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const RingRef rr = (r + k < r1) ? ring[r + k] : RingRef{0, 0};
+            idx[k] = (size_t)rr.node * L + z0;
+            lev[k] = rr.lev;
+        }
+        real lo[kBatch][C], tt[kBatch][C];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < lev[k]) {
+                ldv<C>(LO + idx[k], lo[k]);
+                ldv<C>(ttf + idx[k], tt[k]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; c++) lo[k][c] = tt[k][c] = 0.;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                if (z0 + c < lev[k]) {
+                    vx[c] = RMAX(vx[c], RMAX(lo[k][c], tt[k][c]));
+                    vn[c] = RMIN(vn[c], RMIN(lo[k][c], tt[k][c]));
+                }
+    }
+}
+
+// Gather the fct_adf_h levels z0..z0+C-1 of a node's edges (CSR slice [e0, e1), ascending edge
+// order) and hand each (value, second-endpoint flag) to `f(c, h, second)` in that order.
+template <int C, class F>
+__device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                          const real *__restrict__ adf_h, int z0, int L, F &&f)
 {
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
         size_t idx[kBatch];
@@ -449,181 +490,247 @@ __device__ __forceinline__ void edge_sums(const EdgeRef *__restrict__ edges, int
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             const EdgeRef er = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0};
-            idx[k] = (size_t)er.edge * L + z;
+            idx[k] = (size_t)er.edge * L + z0;
             code[k] = er.code;
         }
-        real h[kBatch];
+        real h[kBatch][C];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) h[k] = (z < (code[k] >> 1)) ? adf_h[idx[k]] : 0.;
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < (code[k] >> 1)) {
+                ldv<C>(adf_h + idx[k], h[k]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; c++) h[k][c] = 0.;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kBatch; k++)
-            if (z < (code[k] >> 1)) {
-                if (code[k] & 1) {
-                    p += RMAX(0., -h[k]);
-                    m += RMIN(0., -h[k]);
-                } else {
-                    p += RMAX(0., h[k]);
-                    m += RMIN(0., h[k]);
-                }
-            }
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                if (z0 + c < (code[k] >> 1)) f(c, h[k][c], code[k] & 1);
     }
 }
 
-// Phase 1: a1 + a2 + a3 + b1v + b1h + b2 for G node columns per block.  Before the barrier every
-// thread issues all of its loads (cluster gathers for tvert, edge gathers for b1h, its own column);
-// after it the vertical 3-point stencil of tvert is read from LDS and the limiter ratios stored.
-template <int VLIMIT>
-__global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invL)
+// Phase 1: a1 + a2 + a3 + b1v + b1h + b2.  Before the barrier every thread issues all of its loads
+// (cluster gathers for tvert, edge gathers for b1h, its own column); after it the vertical 3-point
+// stencil of tvert is read from LDS and the limiter ratios are stored.
+template <int VLIMIT, int C>
+__global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];
-    const int L = a.nl - 1;
+    const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
-    int j, z;
-    cell_of(t, L, invL, j, z);
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
     const int k = block_tile() * G + j;
     const bool col = j < G && k < a.n_owned;
     NodeInfo ni{};
     if (col) ni = mp.node_info[k];
-    const bool wet = col && z < ni.Ln;
-    real vx = 0., vn = 0., p = 0., m = 0., lo = 0., ai = 0.;
+    const int Ln = ni.Ln;
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;  // wet cells of this thread
+    real vx[C], vn[C], p[C], m[C], lo[C], ai[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = lo[c] = ai[c] = 0.;
     size_t b = 0;
-    if (wet) {
-        b = (size_t)ni.n * L + z;
-        const size_t ab = (size_t)ni.n * a.nl + z;
-        lo = a.LO[b];
-        ai = a.area_inv[ab];
-        const real v0 = a.adf_v[ab], v1 = a.adf_v[ab + 1];
-        cluster_bound(mp.p_ring, ni.r0, ni.r1, a.LO, a.ttf, z, L, z >= ni.zdry, a.big, vx, vn);
-        p = RMAX(0., v0) + RMAX(0., -v1);
-        m = RMIN(0., v0) + RMIN(0., -v1);
-        edge_sums(mp.p_edges, ni.e0, ni.e1, a.adf_h, z, L, p, m);
+    if (nw > 0) {
+        b = (size_t)ni.n * L + z0;
+        const size_t ab = (size_t)ni.n * a.nl + z0;
+        ldv<C>(a.LO + b, lo);
+        real v[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? a.adf_v[ab + c] : 0.;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
+            p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
+            m[c] = RMIN(0., v[c]) + RMIN(0., -v[c + 1]);
+        }
+        cluster_bound<C>(mp.p_ring, ni.r0, ni.r1, a.LO, a.ttf, z0, L, ni.zdry, a.big, vx, vn);
+        for_edges<C>(mp.p_edges, ni.e0, ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+            if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
+                p[c] += RMAX(0., -h);
+                m[c] += RMIN(0., -h);
+            } else {
+                p[c] += RMAX(0., h);
+                m[c] += RMIN(0., h);
+            }
+        });
     }
     real *tvx = lds, *tvn = lds + G * L;
-    if (t < G * L) {
-        tvx[t] = vx;
-        tvn[t] = vn;
+    const int q = j * L + z0;
+    if (j < G) {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            tvx[q + c] = vx[c];
+            tvn[q + c] = vn[c];
+        }
     }
     __syncthreads();
-    if (!wet) return;
-    const int Ln = ni.Ln;
-    real tm, tn;
-    if (VLIMIT == 1) {
-        if (z == 0 || z == Ln - 1) {
-            tm = tvx[t];
-            tn = tvn[t];
-        } else {
-            tm = RMAX(RMAX(tvx[t - 1], tvx[t]), tvx[t + 1]);
-            tn = RMIN(RMIN(tvn[t - 1], tvn[t]), tvn[t + 1]);
-        }
-    } else {
-        tm = tvx[t];
-        tn = tvn[t];
-        if (z >= 1 && z < Ln - 1) {
-            const real c0 = RMAX(a.LO[b - 1], a.ttf[b - 1]);
-            const real c1 = RMAX(lo, a.ttf[b]);
-            const real c2 = RMAX(a.LO[b + 1], a.ttf[b + 1]);
-            const real hmx = RMAX(RMAX(c0, c1), c2);
-            const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
-            if (VLIMIT == 2) {
-                tm = RMAX(tm, hmx);
-                tn = RMIN(tn, hmn);
+    if (nw == 0) return;
+    real op[C], om[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        op[c] = om[c] = 0.;
+        const int z = z0 + c;
+        if (c >= nw) continue;
+        real tm, tn;
+        if (VLIMIT == 1) {
+            if (z == 0 || z == Ln - 1) {
+                tm = tvx[q + c];
+                tn = tvn[q + c];
             } else {
-                tm = RMIN(tm, hmx);
-                tn = RMAX(tn, hmn);
+                tm = RMAX(RMAX(tvx[q + c - 1], tvx[q + c]), tvx[q + c + 1]);
+                tn = RMIN(RMIN(tvn[q + c - 1], tvn[q + c]), tvn[q + c + 1]);
+            }
+        } else {
+            tm = tvx[q + c];
+            tn = tvn[q + c];
+            if (z >= 1 && z < Ln - 1) {
+                const size_t bz = b + c;
+                const real c0 = RMAX(a.LO[bz - 1], a.ttf[bz - 1]);
+                const real c1 = RMAX(a.LO[bz], a.ttf[bz]);
+                const real c2 = RMAX(a.LO[bz + 1], a.ttf[bz + 1]);
+                const real hmx = RMAX(RMAX(c0, c1), c2);
+                const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
+                if (VLIMIT == 2) {
+                    tm = RMAX(tm, hmx);
+                    tn = RMIN(tn, hmn);
+                } else {
+                    tm = RMIN(tm, hmx);
+                    tn = RMAX(tn, hmn);
+                }
             }
         }
+        real flux = p[c] * a.dt * ai[c] + a.eps;  // b2, reference.cpp:432-435
+        op[c] = RMIN(1., (tm - lo[c]) / flux);
+        flux = m[c] * a.dt * ai[c] - a.eps;
+        om[c] = RMIN(1., (tn - lo[c]) / flux);
     }
-    real flux = p * a.dt * ai + a.eps;  // reference.cpp:432-435
-    a.plus[b] = RMIN(1., (tm - lo) / flux);
-    flux = m * a.dt * ai - a.eps;
-    a.minus[b] = RMIN(1., (tn - lo) / flux);
+    stv<C>(a.plus + b, op, nw);
+    stv<C>(a.minus + b, om, nw);
 }
 
 // Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
+template <int C>
 __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, int n_edges, int L,
-                                                int G, float invL, const real *__restrict__ plus,
+                                                int G, float invS, const real *__restrict__ plus,
                                                 const real *__restrict__ minus,
                                                 real *__restrict__ adf_h)
 {
-    int j, z;
-    cell_of(threadIdx.x, L, invL, j, z);
+    int j, u;
+    slot_of(threadIdx.x, L / C, invS, j, u);
+    const int z0 = C * u;
     const int k = block_tile() * G + j;
     if (j >= G || k >= n_edges) return;
     const int4 ei = einfo[k];  // {node1, node2, lev, edge}
-    if (z >= ei.z) return;
-    const size_t i = (size_t)ei.w * L + z;
-    const size_t i1 = (size_t)ei.x * L + z, i2 = (size_t)ei.y * L + z;
-    const real f = adf_h[i];
-    adf_h[i] = b3h_factor(f, plus[i1], minus[i1], plus[i2], minus[i2]) * f;
+    const int nw = min(C, ei.z - z0);
+    if (nw <= 0) return;
+    const size_t i = (size_t)ei.w * L + z0;
+    const size_t i1 = (size_t)ei.x * L + z0, i2 = (size_t)ei.y * L + z0;
+    real f[C], p1[C], m1[C], p2[C], m2[C], out[C];
+    ldv<C>(adf_h + i, f);
+    ldv<C>(plus + i1, p1);
+    ldv<C>(minus + i1, m1);
+    ldv<C>(plus + i2, p2);
+    ldv<C>(minus + i2, m2);
+#pragma unroll
+    for (int c = 0; c < C; c++) out[c] = b3h_factor(f[c], p1[c], m1[c], p2[c], m2[c]) * f[c];
+    stv<C>(adf_h + i, out, nw);
 }
 
 // Phase 2, nodes: b3v + cv + ch, G node columns per block.  fct_adf_h already holds the b3-limited
-// fluxes (k_b3h_g ran first, as in docs/refactoring.md:237-314).  The limited vertical flux of
-// interface z+1 is recomputed in-thread from plus/minus(z, z+1) (the bottom interface nlev-1 is
-// never limited); the barrier orders every raw fct_adf_v read of the block before its writes.
-__global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invL)
+// fluxes (k_b3h_g ran first, as in docs/refactoring.md:237-314).  The limited vertical flux of the
+// interface below a thread's levels is recomputed in-thread from plus/minus (the bottom interface
+// nlev-1 is never limited); the barrier orders every raw fct_adf_v read of the block before its
+// writes.
+template <int C>
+__global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
-    const int L = a.nl - 1;
+    const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
-    int j, z;
-    cell_of(t, L, invL, j, z);
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
     const int k = block_tile() * G + j;
     const bool col = j < G && k < a.count;
     NodeInfo ni{};
     if (col) ni = a.nodes[k];
     const int Ln = ni.Ln;
-    const bool act = col && z < (Ln > 1 ? Ln : 1);  // the Fortran always limits nz = 1
-    const bool wet = col && z < Ln;
-    real l0 = 0., dv = 0., dh = 0.;
+    const int top = Ln > 1 ? Ln : 1;                   // the Fortran always limits nz = 1
+    const int na = col ? max(0, min(C, top - z0)) : 0;  // cells whose adf_v is limited
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;   // wet cells (c-step)
+    real l[C], dv[C], dh[C];
     size_t b = 0, ab = 0;
-    if (act) {
-        b = (size_t)ni.n * L + z;
-        ab = (size_t)ni.n * a.nl + z;
-        const real pz = a.plus[b], mz = a.minus[b];
-        const real pm = z ? a.plus[b - 1] : 0., mm = z ? a.minus[b - 1] : 0.;
-        const bool below = z + 1 < Ln;
-        const real pz1 = below ? a.plus[b + 1] : 0., mz1 = below ? a.minus[b + 1] : 0.;
-        const real f0 = a.adf_v[ab], f1 = a.adf_v[ab + 1];
-        l0 = b3v_factor(z, f0, pm, mm, pz, mz) * f0;
-        if (wet) {
-            const real l1 = below ? b3v_factor(z + 1, f1, pz, mz, pz1, mz1) * f1 : f1;
-            const real dta = a.dt / a.area[ab];
-            dv = a.del_v[b] - a.ttf[b] * a.hnode[b];
-            dv = dv + a.LO[b] * a.hnode_new[b];
-            dv = dv + (l0 - l1) * dta;
-            dh = a.del_h[b];
-            for (int k0 = ni.e0; k0 < ni.e1; k0 += kBatch) {
-                size_t idx[kBatch];
-                int code[kBatch];
+    if (na > 0) {
+        b = (size_t)ni.n * L + z0;
+        ab = (size_t)ni.n * a.nl + z0;
+        // plus/minus at z0-1 .. z0+C, fct_adf_v at z0 .. z0+C
+        real pp[C + 2], mm[C + 2], f[C + 1];
+        pp[0] = z0 ? a.plus[b - 1] : 0.;
+        mm[0] = z0 ? a.minus[b - 1] : 0.;
+        {
+            real tp[C], tmn[C];
+            ldv<C>(a.plus + b, tp);
+            ldv<C>(a.minus + b, tmn);
 #pragma unroll
-                for (int q = 0; q < kBatch; q++) {
-                    const EdgeRef er = (k0 + q < ni.e1) ? mp.p_edges[k0 + q] : EdgeRef{0, 0};
-                    idx[q] = (size_t)er.edge * L + z;
-                    code[q] = er.code;
-                }
-                real h[kBatch];
-#pragma unroll
-                for (int q = 0; q < kBatch; q++) h[q] = (z < (code[q] >> 1)) ? a.adf_h[idx[q]] : 0.;
-#pragma unroll
-                for (int q = 0; q < kBatch; q++)  // ascending edge order (docs/refactoring.md:303-314)
-                    if (z < (code[q] >> 1)) dh = (code[q] & 1) ? dh - h[q] * dta : dh + h[q] * dta;
+            for (int c = 0; c < C; c++) {
+                pp[c + 1] = tp[c];
+                mm[c + 1] = tmn[c];
             }
+        }
+        const bool below = z0 + C < Ln;
+        pp[C + 1] = below ? a.plus[b + C] : 0.;
+        mm[C + 1] = below ? a.minus[b + C] : 0.;
+#pragma unroll
+        for (int c = 0; c <= C; c++) f[c] = a.adf_v[ab + c];
+        real lim[C + 1];  // limited adf_v at z0 .. z0+C (raw where not limited)
+#pragma unroll
+        for (int c = 0; c <= C; c++) {
+            const int z = z0 + c;
+            const bool lim_here = (c < C) ? (z < top) : (z < Ln);
+            lim[c] = lim_here ? b3v_factor(z, f[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) * f[c] : f[c];
+        }
+#pragma unroll
+        for (int c = 0; c < C; c++) l[c] = lim[c];
+        if (nw > 0) {
+            real del_v[C], ttf[C], hn[C], lo[C], hnn[C];
+            ldv<C>(a.del_v + b, del_v);
+            ldv<C>(a.ttf + b, ttf);
+            ldv<C>(a.hnode + b, hn);
+            ldv<C>(a.LO + b, lo);
+            ldv<C>(a.hnode_new + b, hnn);
+            ldv<C>(a.del_h + b, dh);
+            real dta[C];
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                dta[c] = c < nw ? a.dt / a.area[ab + c] : 0.;
+                real tv = del_v[c] - ttf[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
+                tv = tv + lo[c] * hnn[c];
+                dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
+            }
+            for_edges<C>(mp.p_edges, ni.e0, ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+                dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+            });
         }
     }
     __syncthreads();
-    if (!act) return;
-    a.adf_v[ab] = l0;
-    if (!wet) return;
-    a.del_v[b] = dv;
-    a.del_h[b] = dh;
+    if (na <= 0) return;
+#pragma unroll
+    for (int c = 0; c < C; c++)
+        if (c < na) a.adf_v[ab + c] = l[c];
+    if (nw <= 0) return;
+    stv<C>(a.del_v + b, dv, nw);
+    stv<C>(a.del_h + b, dh, nw);
 }
 
-int group_columns(int L)
+// columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads)
+int group_columns(int S)
 {
     int best = 1;
     double best_waste = 1e30;
-    for (int G = 1; G * L <= 1024; G *= 2) {
-        const double waste = (double)(((G * L + kWave - 1) / kWave) * kWave) / (G * L);
+    for (int G = 1; G * S <= 1024; G *= 2) {
+        const double waste = (double)(((G * S + kWave - 1) / kWave) * kWave) / (G * S);
         if (waste < best_waste - 1e-9) {
             best_waste = waste;
             best = G;
@@ -633,7 +740,15 @@ int group_columns(int L)
     return best;
 }
 
-static inline unsigned threads_for(int G, int L) { return (unsigned)(((G * L + kWave - 1) / kWave) * kWave); }
+static inline unsigned threads_for(int G, int S) { return (unsigned)(((G * S + kWave - 1) / kWave) * kWave); }
+
+// levels per thread: 2 when columns are 16-byte aligned (L even), else 1
+static inline int levels_per_thread(int L)
+{
+    const char *e = getenv("FESOM2_CPT");
+    if (e && atoi(e) == 1) return 1;
+    return (L % 2 == 0) ? 2 : 1;
+}
 
 // ============================================================================ halo pack / unpack
 
@@ -766,28 +881,37 @@ hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const rea
 
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
-    const int L = a.nl - 1, G = group_columns(L);
-    const float invL = 1.0f / (float)L;
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const float invS = 1.0f / (float)S;
     const long groups = (a.n_owned + G - 1) / G;
     const size_t lds = 2 * (size_t)G * L * sizeof(real);
-    if (a.vlimit == 2) F2A_LAUNCH_GROUPS(k_p1<2>, groups, G, L, lds, s, mp, a, G, invL);
-    if (a.vlimit == 3) F2A_LAUNCH_GROUPS(k_p1<3>, groups, G, L, lds, s, mp, a, G, invL);
-    F2A_LAUNCH_GROUPS(k_p1<1>, groups, G, L, lds, s, mp, a, G, invL);
+    if (C == 2) {
+        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2>), groups, G, S, lds, s, mp, a, G, invS);
+        if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1>), groups, G, S, lds, s, mp, a, G, invS);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 1>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p1<1, 1>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
-    const int L = a.nl - 1, G = group_columns(L);
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (a.count + G - 1) / G;
-    F2A_LAUNCH_GROUPS(k_p2, groups, G, L, 0, s, mp, a, G, 1.0f / (float)L);
+    if (C == 2) F2A_LAUNCH_GROUPS(k_p2<2>, groups, G, S, 0, s, mp, a, G, 1.0f / (float)S);
+    F2A_LAUNCH_GROUPS(k_p2<1>, groups, G, S, 0, s, mp, a, G, 1.0f / (float)S);
 }
 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
                             real *adf_h, hipStream_t s)
 {
-    const int L = nl - 1, G = group_columns(L);
+    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (mp.n_edges + G - 1) / G;
-    F2A_LAUNCH_GROUPS(k_b3h_g, groups, G, L, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)L, plus, minus,
+    if (C == 2)
+        F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)S, plus,
+                          minus, adf_h);
+    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)S, plus, minus,
                       adf_h);
 }
 
