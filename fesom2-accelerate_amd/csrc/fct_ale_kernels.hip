@@ -36,6 +36,9 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 // Bijective XCD-aware swizzle: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // residue class a contiguous range of tiles.  Speed only, never correctness.
 __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements)
+// FESOM2_ABLATE (timing-only builds of an experiment, results are wrong): bit 0 skips the cluster
+// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2.
+__constant__ int c_ablate = 0;
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
 {
@@ -53,6 +56,11 @@ static void init_swizzle()
     if (e && atoi(e) == 0) {
         const int zero = 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_xcd_swizzle), &zero, sizeof zero);
+    }
+    const char *ab = getenv("FESOM2_ABLATE");
+    if (ab && atoi(ab)) {
+        const int v = atoi(ab);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ablate), &v, sizeof v);
     }
 }
 
@@ -395,7 +403,6 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // what lets neighbouring columns' gathers hit its L2.  Columns never straddle blocks, so the LDS
 // stencil of phase 1 and the in-place fct_adf_v update of phase 2 only need block barriers.
 
-static constexpr int kBatch = 8;
 
 // t -> (column j, slot u) for t < G*S (S slots per column), exact: the float quotient stays far
 // from an integer
@@ -407,15 +414,19 @@ __device__ __forceinline__ void slot_of(int t, int S, float invS, int &j, int &u
 
 __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
 
+// C consecutive levels; C even reads 16-byte pairs (p 16-byte aligned)
 template <int C>
 __device__ __forceinline__ void ldv(const real *__restrict__ p, real (&v)[C])
 {
     if constexpr (C == 1) {
         v[0] = p[0];
     } else {
-        const double2 t = *reinterpret_cast<const double2 *>(p);
-        v[0] = t.x;
-        v[1] = t.y;
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+            const double2 t = *reinterpret_cast<const double2 *>(p + c);
+            v[c] = t.x;
+            v[c + 1] = t.y;
+        }
     }
 }
 
@@ -426,16 +437,19 @@ __device__ __forceinline__ void stv(real *__restrict__ p, const real (&v)[C], in
     if constexpr (C == 1) {
         p[0] = v[0];
     } else {
-        if (n == 2)
-            *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
-        else
-            p[0] = v[0];
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+            if (c + 2 <= n)
+                *reinterpret_cast<double2 *>(p + c) = make_double2(v[c], v[c + 1]);
+            else if (c < n)
+                p[c] = v[c];
+        }
     }
 }
 
 // tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
 // straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
-template <int C>
+template <int C, int kBatch>
 __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
                                               const real *__restrict__ LO,
                                               const real *__restrict__ ttf, int z0, int L, int zdry,
@@ -480,7 +494,7 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
 
 // Gather the fct_adf_h levels z0..z0+C-1 of a node's edges (CSR slice [e0, e1), ascending edge
 // order) and hand each (value, second-endpoint flag) to `f(c, h, second)` in that order.
-template <int C, class F>
+template <int C, int kBatch, class F>
 __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
                                           const real *__restrict__ adf_h, int z0, int L, F &&f)
 {
@@ -514,7 +528,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
 // Phase 1: a1 + a2 + a3 + b1v + b1h + b2.  Before the barrier every thread issues all of its loads
 // (cluster gathers for tvert, edge gathers for b1h, its own column); after it the vertical 3-point
 // stencil of tvert is read from LDS and the limiter ratios are stored.
-template <int VLIMIT, int C>
+template <int VLIMIT, int C, int RB, int EB>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];
@@ -529,25 +543,24 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     if (col) ni = mp.node_info[k];
     const int Ln = ni.Ln;
     const int nw = col ? max(0, min(C, Ln - z0)) : 0;  // wet cells of this thread
-    real vx[C], vn[C], p[C], m[C], lo[C], ai[C];
+    real vx[C], vn[C], p[C], m[C];
 #pragma unroll
-    for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = lo[c] = ai[c] = 0.;
-    size_t b = 0;
+    for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = 0.;
+    size_t b = 0, ab = 0;
     if (nw > 0) {
         b = (size_t)ni.n * L + z0;
-        const size_t ab = (size_t)ni.n * a.nl + z0;
-        ldv<C>(a.LO + b, lo);
+        ab = (size_t)ni.n * a.nl + z0;
         real v[C + 1];
 #pragma unroll
         for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? a.adf_v[ab + c] : 0.;
 #pragma unroll
         for (int c = 0; c < C; c++) {
-            ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
             p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
             m[c] = RMIN(0., v[c]) + RMIN(0., -v[c + 1]);
         }
-        cluster_bound<C>(mp.p_ring, ni.r0, ni.r1, a.LO, a.ttf, z0, L, ni.zdry, a.big, vx, vn);
-        for_edges<C>(mp.p_edges, ni.e0, ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+        const int ablate = c_ablate;
+        cluster_bound<C, RB>(mp.p_ring, ni.r0, (ablate & 1) ? ni.r0 : ni.r1, a.LO, a.ttf, z0, L, ni.zdry, a.big, vx, vn);
+        for_edges<C, EB>(mp.p_edges, ni.e0, (ablate & 2) ? ni.e0 : ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
                 m[c] += RMIN(0., -h);
@@ -568,7 +581,10 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     }
     __syncthreads();
     if (nw == 0) return;
-    real op[C], om[C];
+    real lo[C], ai[C], op[C], om[C];
+    ldv<C>(a.LO + b, lo);
+#pragma unroll
+    for (int c = 0; c < C; c++) ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
 #pragma unroll
     for (int c = 0; c < C; c++) {
         op[c] = om[c] = 0.;
@@ -644,7 +660,7 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 // interface below a thread's levels is recomputed in-thread from plus/minus (the bottom interface
 // nlev-1 is never limited); the barrier orders every raw fct_adf_v read of the block before its
 // writes.
-template <int C>
+template <int C, int KB>
 __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
     const int L = a.nl - 1, S = L / C;
@@ -709,7 +725,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
                 tv = tv + lo[c] * hnn[c];
                 dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
             }
-            for_edges<C>(mp.p_edges, ni.e0, ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+            for_edges<C, KB>(mp.p_edges, ni.e0, (c_ablate & 4) ? ni.e0 : ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
                 dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
             });
         }
@@ -879,40 +895,62 @@ hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const rea
         return hipGetLastError();                                                                       \
     } while (0)
 
+static int env_int(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+template <int C, int RB, int EB>
+static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, int G, int S, long groups)
+{
+    const float invS = 1.0f / (float)S;
+    const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real);
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
-    const float invS = 1.0f / (float)S;
     const long groups = (a.n_owned + G - 1) / G;
-    const size_t lds = 2 * (size_t)G * L * sizeof(real);
-    if (C == 2) {
-        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2>), groups, G, S, lds, s, mp, a, G, invS);
-        if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p1<1, 2>), groups, G, S, lds, s, mp, a, G, invS);
+    // batch sizes of the cluster / edge gathers (FESOM2_P1_BATCH = 10*RB + EB; measured)
+    switch (env_int("FESOM2_P1_BATCH", 22)) {
+    case 44: return C == 2 ? p1_launch<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch<1, 4, 4>(mp, a, s, G, S, groups);
+    case 24: return C == 2 ? p1_launch<2, 2, 4>(mp, a, s, G, S, groups) : p1_launch<1, 2, 4>(mp, a, s, G, S, groups);
+    case 42: return C == 2 ? p1_launch<2, 4, 2>(mp, a, s, G, S, groups) : p1_launch<1, 4, 2>(mp, a, s, G, S, groups);
+    case 88: return C == 2 ? p1_launch<2, 8, 8>(mp, a, s, G, S, groups) : p1_launch<1, 8, 8>(mp, a, s, G, S, groups);
+    default: return C == 2 ? p1_launch<2, 2, 2>(mp, a, s, G, S, groups) : p1_launch<1, 2, 2>(mp, a, s, G, S, groups);
     }
-    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1>), groups, G, S, lds, s, mp, a, G, invS);
-    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 1>), groups, G, S, lds, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p1<1, 1>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (a.count + G - 1) / G;
-    if (C == 2) F2A_LAUNCH_GROUPS(k_p2<2>, groups, G, S, 0, s, mp, a, G, 1.0f / (float)S);
-    F2A_LAUNCH_GROUPS(k_p2<1>, groups, G, S, 0, s, mp, a, G, 1.0f / (float)S);
+    const float invS = 1.0f / (float)S;
+    const int KB = env_int("FESOM2_P2_BATCH", 8);
+    if (C == 2) {
+        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8>), groups, G, S, 0, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2<2, 4>), groups, G, S, 0, s, mp, a, G, invS);
+    }
+    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8>), groups, G, S, 0, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2<1, 4>), groups, G, S, 0, s, mp, a, G, invS);
 }
 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
                             real *adf_h, hipStream_t s)
 {
-    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = nl - 1;
+    int C = levels_per_thread(L);
+    if (C == 2 && L % 4 == 0 && env_int("FESOM2_B3H_CPT", 2) == 4) C = 4;  // 4 levels: 2 x 16 B per array
+    const int S = L / C, G = group_columns(S);
     const long groups = (mp.n_edges + G - 1) / G;
-    if (C == 2)
-        F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)S, plus,
-                          minus, adf_h);
-    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, 1.0f / (float)S, plus, minus,
-                      adf_h);
+    const float invS = 1.0f / (float)S;
+    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
+    if (C == 2) F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
+    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
 }
 
 hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,
