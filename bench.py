@@ -90,6 +90,49 @@ def build_local(args, rank, world):
     return m, halo
 
 
+def verify(args, e, step, m, f, rank, world, dist):
+    """One pass on the pristine inputs, owned results gathered on rank 0 and compared cell for cell
+    with the oracle's single-domain pass over the global mesh."""
+    for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+        e.upload(name)  # the host arrays were never touched in resident mode
+    step()
+    abi.device_sync()
+    L = m.L
+    mine = {"gid": m.node_gid[: m.N], "egid": m.edge_gid,
+            "plus": e.download("plus").reshape(-1, L)[: m.N], "minus": e.download("minus").reshape(-1, L)[: m.N],
+            "del_v": e.download("del_v").reshape(-1, L)[: m.N], "del_h": e.download("del_h").reshape(-1, L)[: m.N],
+            "adf_v": e.download("adf_v").reshape(-1, m.nl)[: m.N], "adf_h": e.download("adf_h").reshape(-1, L)}
+    if dist is not None:
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+    else:
+        parts = [mine]
+    if rank != 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nx, ny, nl = synth.CONFIGS[args.config]
+    g = synth.make_mesh(nx, ny * world, nl, full_depth=not args.parity_levels)
+    want = O.full_pass(g, synth.make_fields(g))
+    wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
+    bad = {}
+    for p in parts:
+        gid = p["gid"]
+        for k in ("plus", "minus"):
+            w = want[k].reshape(-1, L)[gid]
+            n = int(np.sum((p[k] != w) & wet[gid]))
+            if n:
+                bad[k] = bad.get(k, 0) + n
+        for k, stride in (("del_v", L), ("del_h", L), ("adf_v", nl)):
+            n = int(np.sum(p[k] != want[k].reshape(-1, stride)[gid]))
+            if n:
+                bad[k] = bad.get(k, 0) + n
+        n = int(np.sum(p["adf_h"] != want["adf_h"].reshape(-1, L)[p["egid"]]))
+        if n:
+            bad["adf_h"] = bad.get("adf_h", 0) + n
+    return {"exact": not bad, "mismatched_cells": bad, "against": "oracle full pass on the global mesh"}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,6 +143,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
     ap.add_argument("--path", default="fused", choices=["fused", "stepwise"])
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
+                         "oracle on the global mesh (gathered over ranks)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
     args = ap.parse_args()
@@ -253,6 +299,10 @@ def main():
                "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
                          f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)"}
 
+    check = None
+    if args.check:
+        check = verify(args, e, step, m, f, rank, world, dist)
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "cell-updates/s", "n_gpus": world,
@@ -274,6 +324,8 @@ def main():
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "setup_s": round(setup_s, 1),
         }
+        if check is not None:
+            out["check"] = check
         print(json.dumps(out), flush=True)
 
     e.free()

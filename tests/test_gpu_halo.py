@@ -1,0 +1,116 @@
+"""GPU: the in-library RCCL halo exchange (fct_ale_exchange_acc_).
+
+RCCL refuses two ranks on one device, so a one-GPU box cannot run the multi-rank exchange; here a
+one-rank communicator exchanges with itself (grouped ncclSend/ncclRecv to rank 0 are legal), which
+runs the whole pack -> send/recv -> unpack path with several neighbour slots and their buffer
+offsets.  The multi-rank data flow itself (lists, ordering, equality with the single-domain pass) is
+covered on the CPU by tests/test_partition.py (gloo, world_size 2) and on the GPU by
+test_gpu_parity.py::test_partitioned_pass_on_one_gpu; bench.py --check verifies N > 1 runs.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from fesom2_amd import abi
+from fesom2_amd.abi import arr, dll, ip
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm():
+    abi.set_mpi_rank(0, 1)
+    uid = (C.c_char * 128)()
+    st = C.c_int(0)
+    dll().fesom2_comm_unique_id_(uid, C.byref(st))
+    abi.check(st, "fesom2_comm_unique_id_")
+    h = abi.Handle("comm")
+    dll().fesom2_comm_init_(h.ref, uid, ip(0), ip(1), C.byref(st))
+    abi.check(st, "fesom2_comm_init_")
+    yield h
+    dll().fesom2_comm_free_(h.ref)
+
+
+def make_buffer(values):
+    h = abi.Handle("buf")
+    st = C.c_int(0)
+    dll().alloc_var_(h.ref, None, ip(values.size), abi.bp(False), C.byref(st))
+    abi.check(st, "alloc_var_")
+    dll().fesom2_upload_(h.ref, arr(values), C.byref(st))
+    abi.check(st, "upload")
+    return h
+
+
+def download(h, n):
+    out = np.empty(n)
+    st = C.c_int(0)
+    dll().fesom2_download_(h.ref, arr(out), C.byref(st))
+    abi.check(st, "download")
+    return out
+
+
+def make_plan(ranks, send, recv, nl):
+    h = abi.Handle("plan")
+    st = C.c_int(0)
+    sc = np.array([len(s) for s in send], np.int32)
+    rc = np.array([len(r) for r in recv], np.int32)
+    sn = np.ascontiguousarray(np.concatenate(send).astype(np.int32))
+    rn = np.ascontiguousarray(np.concatenate(recv).astype(np.int32))
+    dll().fesom2_halo_plan_(h.ref, ip(len(ranks)), arr(np.array(ranks, np.int32)), arr(sc), arr(sn), arr(rc),
+                            arr(rn), ip(nl), C.byref(st))
+    return h, st.value
+
+
+def test_self_exchange_moves_columns(comm):
+    L, ncol = 20, 40
+    z = np.arange(L)
+    plus = (np.arange(ncol)[:, None] * 1000.0 + z[None, :]).reshape(-1)
+    minus = -plus - 0.5
+    bp, bm = make_buffer(plus), make_buffer(minus)
+    # two neighbour slots (both rank 0): columns (1-based) 1,2,3 -> 30,31,32 and 5,6 -> 38,39
+    plan, st = make_plan([0, 0], [[1, 2, 3], [5, 6]], [[30, 31, 32], [38, 39]], L + 1)
+    assert st == 0
+    s = abi.Stream()
+    try:
+        ist = C.c_int(-1)
+        dll().fct_ale_exchange_acc_(C.byref(ist), s.ref, comm.ref, plan.ref, bp.ref, bm.ref)
+        assert ist.value == 0, abi.last_error()
+        s.sync()
+        gp = download(bp, plus.size).reshape(ncol, L)
+        gm = download(bm, minus.size).reshape(ncol, L)
+        want_p = plus.reshape(ncol, L).copy()
+        want_m = minus.reshape(ncol, L).copy()
+        for src, dst in ((0, 29), (1, 30), (2, 31), (4, 37), (5, 38)):
+            want_p[dst] = want_p[src]
+            want_m[dst] = want_m[src]
+        assert np.array_equal(gp, want_p)
+        assert np.array_equal(gm, want_m)
+    finally:
+        dll().fesom2_halo_plan_free_(plan.ref)
+        dll().fesom2_free_(bp.ref)
+        dll().fesom2_free_(bm.ref)
+        s.free()
+
+
+def test_exchange_rejects_out_of_range_columns(comm):
+    L = 10
+    bp, bm = make_buffer(np.zeros(5 * L)), make_buffer(np.zeros(5 * L))
+    plan, st = make_plan([0], [[1]], [[9]], L + 1)  # column 9 does not exist in a 5-column buffer
+    assert st == 0
+    s = abi.Stream()
+    try:
+        ist = C.c_int(-1)
+        dll().fct_ale_exchange_acc_(C.byref(ist), s.ref, comm.ref, plan.ref, bp.ref, bm.ref)
+        assert ist.value == 1
+        assert "holds" in abi.last_error()
+    finally:
+        dll().fesom2_halo_plan_free_(plan.ref)
+        dll().fesom2_free_(bp.ref)
+        dll().fesom2_free_(bm.ref)
+        s.free()
+
+
+def test_plan_rejects_bad_node_numbers():
+    plan, st = make_plan([0], [[0]], [[1]], 11)  # node numbers are 1-based
+    assert st == 1 and not plan

@@ -199,3 +199,84 @@ def test_full_size_1p2m_x_80():
     st, got = run_pass(m, f)
     assert st == 9
     check_pass(m, got, want)
+
+
+@pytest.mark.parametrize("name", ["tiny_16x8x10", "small_24x12x15"])
+def test_golden_vectors_on_gpu(name):
+    """The committed vectors made by the reference's own code (tests/golden/make_golden.py)."""
+    from test_oracle import load_fixture
+    m, f, want = load_fixture(name)
+    st, got = run_pass(m, f)
+    assert st == 9
+    check_pass(m, got, want)
+
+
+@pytest.mark.parametrize("kind,nranks", [("strips", 2), ("strips", 4), ("random", 3)])
+def test_partitioned_pass_on_one_gpu(kind, nranks):
+    """Halo meshes through the HIP engine: phase 1 per partition, the caller's exchange of
+    fct_plus/fct_minus (here on the host, as the Fortran's exchange_nod does), fused phase 2.
+    Owned results must equal the single-domain oracle exactly."""
+    from fesom2_amd import partition
+    nx, ny, nl = 64, 48, 21
+    g = synth.make_mesh(nx, ny, nl)
+    want = O.full_pass(g, synth.make_fields(g))
+    if kind == "strips":
+        part = partition.strip_parts(nx, ny, nranks)
+    else:
+        part = np.random.default_rng(3).integers(0, nranks, g.N).astype(np.int32)
+    locs = [partition.local_mesh(g, part, r) for r in range(nranks)]
+    runs = []
+    try:
+        for m, _ in locs:
+            dm = engine.DeviceMesh(m)
+            runs.append((dm, engine.FctAle(dm, synth.make_fields(m))))
+        for _, e in runs:
+            assert e.pre_comm() == 6
+        pm = []
+        for _, e in runs:
+            e.sync()
+            pm.append((e.download("plus").reshape(-1, g.L), e.download("minus").reshape(-1, g.L)))
+        for r, (m, h) in enumerate(locs):
+            for q in h.neighbors:
+                src, dst = locs[q][1].send[r] - 1, h.recv[q] - 1
+                pm[r][0][dst] = pm[q][0][src]
+                pm[r][1][dst] = pm[q][1][src]
+            runs[r][1].upload("plus", pm[r][0].reshape(-1))
+            runs[r][1].upload("minus", pm[r][1].reshape(-1))
+        for _, e in runs:
+            assert e.post_comm_c() == 9
+        outs = []
+        for _, e in runs:
+            e.sync()
+            outs.append({k: e.download(k) for k in ("del_v", "del_h", "adf_v")})
+    finally:
+        for dm, e in runs:
+            e.free()
+            dm.free()
+    ms = [m for m, _ in locs]
+    for k in ("del_v", "del_h"):
+        assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r][k], g.L, g.N), want[k]), k
+    assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r]["adf_v"], g.nl, g.N), want["adf_v"])
+    owned_plus = partition.gather_owned(ms, lambda r: pm[r][0].reshape(-1), g.L, g.N)
+    assert_cols_equal(owned_plus, want["plus"], g.nlev_nod, g.L, g.N, "plus")
+
+
+def test_reference_named_entries_run_on_gpu():
+    """fct_ale_a1_reference_ .. fct_ale_pre_comm_ (reference .h:142, :225-235) on host arrays,
+    executed by the HIP engine: same results as reference.cpp's CPU functions."""
+    import ctypes as C
+    from fesom2_amd.abi import arr, dll, dp, ip
+    m, f = mesh("8k x 20")
+    L, NT = m.L, m.N + m.H
+    tmax, tmin, plus, minus = (np.zeros(NT * L) for _ in range(4))
+    UV = np.zeros(2 * L * m.T)
+    st = C.c_int(-1)
+    dll().fct_ale_pre_comm_(C.byref(st), arr(tmax), arr(tmin), arr(plus), arr(minus), arr(f["ttf"]), arr(f["LO"]),
+                            arr(f["adf_v"]), arr(f["adf_h"]), arr(UV), arr(f["area_inv"]), ip(m.N), ip(m.H),
+                            ip(m.T), ip(m.E), ip(m.nl), arr(m.nlev_nod), arr(m.nlev_elem), arr(m.elem2D_nodes),
+                            arr(m.nie_num), arr(m.nie), ip(m.dim), arr(m.edges), arr(m.edge_tri), ip(1), dp(1e-16),
+                            dp(1e3), dp(1.0))
+    assert st.value == 5
+    want = O.pre_comm(m, f)[1]
+    for k, v in (("ttf_max", tmax), ("ttf_min", tmin), ("plus", plus), ("minus", minus), ("UV", UV)):
+        assert np.array_equal(v, want[k]), k

@@ -1,0 +1,152 @@
+"""CPU: the oracle against the reference (reference.cpp build + committed golden vectors).
+
+The oracle (oracle/fct_ale_oracle.c) is the checker of every GPU parity test, so it is pinned first:
+* bit-for-bit against src/reference.cpp compiled from /root/reference (oracle/_ref), when present;
+* bit-for-bit against tests/golden/*.npz and tests/golden/hashes.json, which were produced by the
+  reference's own code (reference.cpp for a1..a4, its numpy reference() functions for b3/c) by
+  tests/golden/make_golden.py -- these travel with the repo, so the pin also holds on the GPU box.
+"""
+import dataclasses
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fesom2_amd import synth
+
+import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def load_fixture(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))  # allow_pickle=False (default)
+    nl, N, H, T, E, dim = (int(v) for v in z["sizes"])
+    m = synth.Mesh(nl=nl, N=N, H=H, T=T, E=E, dim=dim,
+                   **{k: z["mesh_" + k] for k in ("elem2D_nodes", "edges", "edge_tri", "nie_num", "nie",
+                                                  "nlev_elem", "nlev_nod")},
+                   node_gid=np.arange(N + H, dtype=np.int64), edge_gid=np.arange(E, dtype=np.int64), name=name)
+    f = {k[3:]: z[k] for k in z.files if k.startswith("in_")}
+    out = {k[4:]: z[k] for k in z.files if k.startswith("out_")}
+    return m, f, out
+
+
+@pytest.mark.parametrize("name", ["tiny_16x8x10", "small_24x12x15"])
+def test_oracle_matches_golden_vectors(name):
+    m, f, want = load_fixture(name)
+    got = O.full_pass(m, f)
+    for k, w in want.items():
+        assert np.array_equal(got[k].view(np.uint64), w.view(np.uint64)), f"{name}: {k} differs"
+
+
+def test_oracle_matches_golden_hashes_8k_x_20():
+    h = json.load(open(os.path.join(GOLDEN, "hashes.json")))
+    m = synth.config_mesh(h["mesh"])
+    f = synth.make_fields(m)
+    for k, v in h["inputs"].items():
+        assert sha(f[k]) == v, f"synthetic input {k} is not bit-identical to the fixture's"
+    got = O.full_pass(m, f)
+    for k, v in h["outputs"].items():
+        assert sha(got[k]) == v, f"oracle output {k} differs from the reference's"
+
+
+MESHES = [("tiny", False, False), ("8k x 20", False, False), ("8k x 20", True, False), ("8k x 20", False, True)]
+
+
+@pytest.mark.skipif(O.ref() is None, reason="oracle/_ref (reference.cpp build) not present")
+@pytest.mark.parametrize("name,full,perm", MESHES)
+def test_oracle_matches_reference_cpp(name, full, perm):
+    m = synth.config_mesh(name, full_depth=full)
+    if perm:
+        m = synth.permute_mesh(m)
+    f = synth.make_fields(m)
+    st, got = O.pre_comm(m, f)
+    assert st == 5
+    want = O.ref_pre_comm(m, f)
+    for k in ("ttf_max", "ttf_min", "plus", "minus", "UV"):
+        assert np.array_equal(got[k].view(np.uint64), want[k].view(np.uint64)), k
+
+
+def test_vlimit_protocol_of_reference_cpp():
+    """reference.cpp runs a3/a4 only for vlimit == 1 and reports alg_state 2 otherwise (:297-303)."""
+    m = synth.config_mesh("tiny")
+    f = synth.make_fields(m)
+    for vl in (2, 3):
+        st, _ = O.pre_comm(m, f, vlimit=vl, vlimit_ext=False)
+        assert st == 2
+        st, _ = O.pre_comm(m, f, vlimit=vl, vlimit_ext=True)
+        assert st == 5
+
+
+def test_limiter_is_active_on_synthetic_fields():
+    """The synthetic scales must exercise b2/b3 (ratios below 1 in a good share of cells)."""
+    m = synth.config_mesh("8k x 20")
+    f = synth.make_fields(m)
+    _, out = O.pre_comm(m, f)
+    L = m.L
+    wet = np.arange(L)[None, :] < (m.nlev_nod[:, None] - 1)
+    plus = out["plus"].reshape(-1, L)[wet]
+    assert 0.1 < np.mean(plus < 1.0) < 0.9
+    assert plus.min() >= 0.0
+
+
+def test_mesh_generator_conventions():
+    m = synth.config_mesh("8k x 20")
+    nx, ny, nl = synth.CONFIGS["8k x 20"]
+    assert (m.N, m.T, m.E) == (nx * ny, 2 * nx * (ny - 1), 3 * nx * (ny - 1) + nx)
+    en = m.elem2D_nodes.reshape(-1, 3) - 1
+    # nlevels_nod2D = max over adjacent elements
+    mx = np.zeros(m.N, np.int32)
+    np.maximum.at(mx, en.reshape(-1), np.repeat(m.nlev_elem, 3))
+    assert np.array_equal(mx, m.nlev_nod)
+    assert m.nlev_elem.min() >= 3 and m.nlev_elem.max() <= nl
+    # every edge's first element contains both endpoints; second is 0 only on the y boundary
+    ed = m.edges.reshape(-1, 2) - 1
+    et = m.edge_tri.reshape(-1, 2)
+    assert (et[:, 0] > 0).all()
+    for k in (0, 1):
+        has = et[:, k] > 0
+        tri = en[et[has, k] - 1]
+        assert ((tri == ed[has, 0:1]).any(1) & (tri == ed[has, 1:2]).any(1)).all()
+    # nod_in_elem2D lists exactly the adjacent elements
+    nie = m.nie.reshape(-1, m.dim)
+    cnt = np.bincount(en.reshape(-1), minlength=m.N)
+    assert np.array_equal(cnt, m.nie_num)
+    assert cnt.max() <= m.dim
+
+
+def test_survey_config_sizes():
+    """SURVEY.md §8 / BASELINE.md: 1.2M x 80 mesh has 2,396,800 elements and 3,596,800 edges."""
+    m = synth.config_mesh("1.2M x 80", full_depth=True)
+    assert (m.N, m.T, m.E, m.L) == (1_200_000, 2_396_800, 3_596_800, 80)
+    assert m.cells == 96_000_000
+
+
+def test_permuted_mesh_describes_the_same_problem():
+    """Renumbering must not change the physics: per-global-id results agree up to the order of the
+    edge sums (renumbered edges are added in a different order, so only rounding may differ)."""
+    m = synth.config_mesh("tiny")
+    p = synth.permute_mesh(m)
+    a = O.full_pass(m, synth.make_fields(m))
+    b = O.full_pass(p, synth.make_fields(p))
+    L = m.L
+    for k in ("plus", "minus", "del_v", "del_h"):
+        A = a[k].reshape(-1, L)[p.node_gid]
+        assert np.allclose(A, b[k].reshape(-1, L), rtol=1e-12, atol=1e-14), k
+    assert np.allclose(a["adf_h"].reshape(-1, L)[p.edge_gid], b["adf_h"].reshape(-1, L), rtol=1e-12, atol=1e-14)
+
+
+def test_empty_edge_set_and_minimum_levels():
+    """Edge cases the reference's loops admit: no edges (b1h/b3h/ch are no-ops), nlevels = 3."""
+    m = synth.make_mesh(4, 2, 3)
+    f = synth.make_fields(m)
+    st, out = O.pre_comm(dataclasses.replace(m, E=0), f)
+    assert st == 5
+    full = O.full_pass(m, f)
+    assert np.isfinite(full["plus"]).all()
