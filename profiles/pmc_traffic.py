@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 PMC passes into HBM bytes per kernel launch (profiles/traffic.json).
+
+Method (MI355X_MICROARCH.md "HBM", calibrated in this repo): FETCH_SIZE reads half of the bytes of
+a coalesced stream on gfx950, so the L2->fabric request counters are used instead.  Calibration on
+the stepwise k_a1 kernel, which reads exactly 2 x 768 MB and writes 2 x 768 MB at 1.2M x 80
+(profiles/r01_calibration_stepwise_*.csv): TCC_EA0_RDREQ_128B_sum = 12.0e6 (x 128 B = 1.536 GB) and
+TCC_EA0_WRREQ_64B_sum = 24.0e6 (x 64 B = 1.536 GB).  So
+
+    read bytes  = 128 * RDREQ_128B + 64 * RDREQ_64B + 32 * RDREQ_32B
+    write bytes = 64 * WRREQ_64B + 32 * (WRREQ - WRREQ_64B)
+
+(the counters include Infinity-Cache hits: this is L2-miss traffic, an upper bound on HBM bytes).
+
+usage: pmc_traffic.py READ_CSV WRITE_CSV WORKLOAD OUT_JSON
+"""
+import collections
+import csv
+import json
+import sys
+
+NAMES = {"k_p1": "fct_ale_p1", "k_p2": "fct_ale_p2", "k_b3h_g": "fct_ale_b3_horizontal"}
+
+
+def per_kernel(path):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("f2a::", "").strip()
+        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    rd, wr, workload, out = sys.argv[1:5]
+    R, W = per_kernel(rd), per_kernel(wr)
+    res = {}
+    for k, name in NAMES.items():
+        if k not in R or k not in W:
+            continue
+        r, w = R[k], W[k]
+        rb = 128 * r.get("TCC_EA0_RDREQ_128B_sum", 0) + 64 * r.get("TCC_EA0_RDREQ_64B_sum", 0) + \
+            32 * r.get("TCC_EA0_RDREQ_32B_sum", 0)
+        wb = 64 * w.get("TCC_EA0_WRREQ_64B_sum", 0) + 32 * (w.get("TCC_EA0_WRREQ_sum", 0) -
+                                                            w.get("TCC_EA0_WRREQ_64B_sum", 0))
+        res[name] = {"read_bytes": int(rb), "write_bytes": int(wb), "total": int(rb + wb)}
+    doc = {"workload": workload, "bytes_per_launch": {k: v["total"] for k, v in res.items()}, "detail": res,
+           "method": __doc__.strip().splitlines()[0] + " -- see profiles/pmc_traffic.py"}
+    json.dump(doc, open(out, "w"), indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
