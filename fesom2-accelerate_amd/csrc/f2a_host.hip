@@ -445,11 +445,20 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
         for (int e = 0; e < n_edges; e++)
             if (!etaken[e]) push_edge(e);
+        std::vector<NodeRec> recs(n_owned);
+        for (int k = 0; k < n_owned; k++) {
+            NodeRec &r = recs[k];
+            memset(&r, 0, sizeof r);
+            r.info = info[k];
+            for (int q = 0; q < kRecRing && info[k].r0 + q < info[k].r1; q++) r.ring[q] = pring[info[k].r0 + q];
+            for (int q = 0; q < kRecEdge && info[k].e0 + q < info[k].e1; q++) r.edge[q] = pedges[info[k].e0 + q];
+        }
+        d.node_rec = plan->mem.upload(recs);
         d.node_info = plan->mem.upload(info);
         d.p_edges = plan->mem.upload(pedges);
         d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.node_info || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
+        if (!d.node_info || !d.node_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
             return fail("device allocation for the processing order failed");
     } else if (n_edges > 0) {
         std::vector<int4> einfo(n_edges);

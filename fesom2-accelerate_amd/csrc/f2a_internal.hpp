@@ -50,6 +50,18 @@ struct NodeInfo {
     int pad;
 };
 
+// NodeInfo plus the first kRecRing cluster and kRecEdge edge entries inline (160 bytes, 16-byte
+// aligned): a block loads its columns' records with one coalesced sweep into LDS, so the gathers
+// depend on a single global load instead of NodeInfo -> CSR -> gather.  Entries beyond the inline
+// capacity stay in the processing-order CSRs at [r0 + kRecRing, r1) / [e0 + kRecEdge, e1).
+constexpr int kRecRing = 8, kRecEdge = 8;
+struct alignas(16) NodeRec {
+    NodeInfo info;
+    RingRef ring[kRecRing];
+    EdgeRef edge[kRecEdge];
+};
+static_assert(sizeof(NodeRec) == 160, "NodeRec layout");
+
 // Device-side view of the derived mesh structures of one (mesh, partition) pair.
 struct MeshPlanDev {
     int n_owned = 0;       // myDim_nod2D
@@ -67,6 +79,7 @@ struct MeshPlanDev {
     // owned nodes and local edges in the order the fused kernels visit them, with the CSRs
     // re-laid out in that order
     const NodeInfo *node_info = nullptr;  // [n_owned]
+    const NodeRec *node_rec = nullptr;    // [n_owned]
     const EdgeRef *p_edges = nullptr;     // node->edge CSR, processing order
     const RingRef *p_ring = nullptr;      // cluster CSR, processing order (if has ring)
     const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order
@@ -87,7 +100,7 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 
 struct P2Args {
     int nl;
-    const NodeInfo *nodes;  // processing positions to run (a subset of the plan's node_info)
+    const NodeRec *nodes;   // processing positions to run (a subset of the plan's node_rec)
     int count;
     const real *plus, *minus, *ttf, *LO, *hnode, *hnode_new, *area;
     real *adf_v, *adf_h, *del_v, *del_h;

@@ -449,18 +449,14 @@ __device__ __forceinline__ void stv(real *__restrict__ p, const real (&v)[C], in
 
 // tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
 // straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
+// (vx, vn must be initialised by the caller: -/+bignumber where an adjacent element is dry, else
+// -/+infinity)
 template <int C, int kBatch>
 __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
                                               const real *__restrict__ LO,
-                                              const real *__restrict__ ttf, int z0, int L, int zdry,
-                                              real big, real (&vx)[C], real (&vn)[C])
+                                              const real *__restrict__ ttf, int z0, int L,
+                                              real (&vx)[C], real (&vn)[C])
 {
-#pragma unroll
-    for (int c = 0; c < C; c++) {
-        const bool dry = z0 + c >= zdry;
-        vx[c] = dry ? -big : -INFINITY;
-        vn[c] = dry ? big : INFINITY;
-    }
     for (int r = r0; r < r1; r += kBatch) {
         size_t idx[kBatch];
         int lev[kBatch];
@@ -528,19 +524,34 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
 // Phase 1: a1 + a2 + a3 + b1v + b1h + b2.  Before the barrier every thread issues all of its loads
 // (cluster gathers for tvert, edge gathers for b1h, its own column); after it the vertical 3-point
 // stencil of tvert is read from LDS and the limiter ratios are stored.
+// The block's NodeRec records (one coalesced 16-byte-per-thread sweep) into LDS after `lds_base`.
+__device__ __forceinline__ const NodeRec *stage_records(const NodeRec *__restrict__ recs, int first, int ncol,
+                                                        real *lds_base)
+{
+    NodeRec *r = reinterpret_cast<NodeRec *>(lds_base);
+    const int4 *src = reinterpret_cast<const int4 *>(recs + first);
+    int4 *dst = reinterpret_cast<int4 *>(r);
+    constexpr int kChunks = sizeof(NodeRec) / sizeof(int4);
+    for (int i = threadIdx.x; i < ncol * kChunks; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    return r;
+}
+
 template <int VLIMIT, int C, int RB, int EB>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
-    extern __shared__ real lds[];
+    extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
     const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
+    const int first = block_tile() * G;
+    const int ncol = min(G, a.n_owned - first);
+    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     int j, u;
     slot_of(t, S, invS, j, u);
     const int z0 = C * u;
-    const int k = block_tile() * G + j;
-    const bool col = j < G && k < a.n_owned;
+    const bool col = j < ncol;
     NodeInfo ni{};
-    if (col) ni = mp.node_info[k];
+    if (col) ni = recs[j].info;
     const int Ln = ni.Ln;
     const int nw = col ? max(0, min(C, Ln - z0)) : 0;  // wet cells of this thread
     real vx[C], vn[C], p[C], m[C];
@@ -559,8 +570,16 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             m[c] = RMIN(0., v[c]) + RMIN(0., -v[c + 1]);
         }
         const int ablate = c_ablate;
-        cluster_bound<C, RB>(mp.p_ring, ni.r0, (ablate & 1) ? ni.r0 : ni.r1, a.LO, a.ttf, z0, L, ni.zdry, a.big, vx, vn);
-        for_edges<C, EB>(mp.p_edges, ni.e0, (ablate & 2) ? ni.e0 : ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+        const int nr = (ablate & 1) ? 0 : ni.r1 - ni.r0, ne = (ablate & 2) ? 0 : ni.e1 - ni.e0;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            const bool dry = z0 + c >= ni.zdry;
+            vx[c] = dry ? -a.big : -INFINITY;
+            vn[c] = dry ? a.big : INFINITY;
+        }
+        cluster_bound<C, RB>(recs[j].ring, 0, min(nr, kRecRing), a.LO, a.ttf, z0, L, vx, vn);
+        if (nr > kRecRing) cluster_bound<C, RB>(mp.p_ring, ni.r0 + kRecRing, ni.r1, a.LO, a.ttf, z0, L, vx, vn);
+        auto add = [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
                 m[c] += RMIN(0., -h);
@@ -568,11 +587,13 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
                 p[c] += RMAX(0., h);
                 m[c] += RMIN(0., h);
             }
-        });
+        };
+        for_edges<C, EB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+        if (ne > kRecEdge) for_edges<C, EB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
     }
     real *tvx = lds, *tvn = lds + G * L;
     const int q = j * L + z0;
-    if (j < G) {
+    if (col) {
 #pragma unroll
         for (int c = 0; c < C; c++) {
             tvx[q + c] = vx[c];
@@ -663,15 +684,18 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 template <int C, int KB>
 __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
+    extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
+    const int first = block_tile() * G;
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
     int j, u;
     slot_of(t, S, invS, j, u);
     const int z0 = C * u;
-    const int k = block_tile() * G + j;
-    const bool col = j < G && k < a.count;
+    const bool col = j < ncol;
     NodeInfo ni{};
-    if (col) ni = a.nodes[k];
+    if (col) ni = recs[j].info;
     const int Ln = ni.Ln;
     const int top = Ln > 1 ? Ln : 1;                   // the Fortran always limits nz = 1
     const int na = col ? max(0, min(C, top - z0)) : 0;  // cells whose adf_v is limited
@@ -725,9 +749,12 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
                 tv = tv + lo[c] * hnn[c];
                 dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
             }
-            for_edges<C, KB>(mp.p_edges, ni.e0, (c_ablate & 4) ? ni.e0 : ni.e1, a.adf_h, z0, L, [&](int c, real h, int second) {
+            const int ne = (c_ablate & 4) ? 0 : ni.e1 - ni.e0;
+            auto add = [&](int c, real h, int second) {
                 dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
-            });
+            };
+            for_edges<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+            if (ne > kRecEdge) for_edges<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
         }
     }
     __syncthreads();
@@ -905,7 +932,7 @@ template <int C, int RB, int EB>
 static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, int G, int S, long groups)
 {
     const float invS = 1.0f / (float)S;
-    const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real);
+    const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real) + (size_t)G * sizeof(NodeRec);
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
@@ -930,13 +957,14 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (a.count + G - 1) / G;
     const float invS = 1.0f / (float)S;
-    const int KB = env_int("FESOM2_P2_BATCH", 8);
+    const int KB = env_int("FESOM2_P2_BATCH", 4);
+    const size_t lds = (size_t)G * sizeof(NodeRec);
     if (C == 2) {
-        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8>), groups, G, S, 0, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2<2, 4>), groups, G, S, 0, s, mp, a, G, invS);
+        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2<2, 4>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8>), groups, G, S, 0, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p2<1, 4>), groups, G, S, 0, s, mp, a, G, invS);
+    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2<1, 4>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,

@@ -312,7 +312,7 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
     if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h_fused(plan->dev, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), st); }))
         return;
     *alg_state = 8;
-    f2a::P2Args a{NL, plan->dev.node_info, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
+    f2a::P2Args a{NL, plan->dev.node_rec, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
                   dptr<real>(blo), dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv),
                   dptr<real>(badfh), dptr<real>(bdv), dptr<real>(bdh), *dt};
     if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(plan->dev, a, st); })) return;
