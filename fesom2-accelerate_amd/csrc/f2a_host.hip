@@ -445,6 +445,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
         for (int e = 0; e < n_edges; e++)
             if (!etaken[e]) push_edge(e);
+        // interior / boundary split for the exchange overlap (stable: processing order kept)
+        auto interior_edge = [&](const int4 &ei) { return ei.x < n_owned && ei.y < n_owned; };
+        std::stable_partition(einfo.begin(), einfo.end(), interior_edge);
+        d.n_edge_interior = (int)std::count_if(einfo.begin(), einfo.end(), interior_edge);
         std::vector<NodeRec> recs(n_owned);
         for (int k = 0; k < n_owned; k++) {
             NodeRec &r = recs[k];
@@ -454,16 +458,25 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             for (int q = 0; q < kRecEdge && info[k].e0 + q < info[k].e1; q++) r.edge[q] = pedges[info[k].e0 + q];
         }
         d.node_rec = plan->mem.upload(recs);
+        std::vector<char> interior_node(n_owned, 1);
+        for (int n = 0; n < n_owned; n++)
+            for (int k = ptr[n]; k < ptr[n + 1]; k++)
+                if (other[k] >= n_owned) interior_node[n] = 0;
+        std::vector<NodeRec> p2(recs);
+        std::stable_partition(p2.begin(), p2.end(), [&](const NodeRec &r) { return interior_node[r.info.n] != 0; });
+        d.n_p2_interior = (int)std::count(interior_node.begin(), interior_node.end(), (char)1);
+        d.p2_rec = plan->mem.upload(p2);
         d.node_info = plan->mem.upload(info);
         d.p_edges = plan->mem.upload(pedges);
         d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.node_info || !d.node_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
+        if (!d.node_info || !d.node_rec || !d.p2_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
             return fail("device allocation for the processing order failed");
     } else if (n_edges > 0) {
         std::vector<int4> einfo(n_edges);
         for (int e = 0; e < n_edges; e++)
             einfo[e] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
+        d.n_edge_interior = n_edges;
         d.p_edge_info = plan->mem.upload(einfo);
         if (!d.p_edge_info) return fail("device allocation for the edge list failed");
     }

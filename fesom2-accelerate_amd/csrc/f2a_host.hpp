@@ -99,4 +99,9 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                      bool with_ring);
 void drop_plans_of(const Buffer *b);
 
+// ---- halo exchange (halo_rccl.hip): enqueue pack -> grouped ncclSend/ncclRecv -> unpack on the
+// halo plan's communication stream after the work already queued on `s`.  Returns an event that
+// completes when the halo columns hold the neighbours' values (nullptr on failure).
+hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *plus, Buffer *minus, hipStream_t s);
+
 }  // namespace f2a

@@ -82,7 +82,13 @@ struct MeshPlanDev {
     const NodeRec *node_rec = nullptr;    // [n_owned]
     const EdgeRef *p_edges = nullptr;     // node->edge CSR, processing order
     const RingRef *p_ring = nullptr;      // cluster CSR, processing order (if has ring)
-    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order
+    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order,
+                                          // interior edges (both endpoints owned) first
+    int n_edge_interior = 0;
+    // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
+    // nodes; interior work needs no halo values, so it can overlap the halo exchange
+    const NodeRec *p2_rec = nullptr;      // [n_owned]
+    int n_p2_interior = 0;
     // local edges with no owned endpoint (b3-horizontal still applies to them)
     const int *orphan_edges = nullptr;
     int n_orphans = 0;
@@ -108,8 +114,8 @@ struct P2Args {
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
-hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
-                            real *adf_h, hipStream_t s);
+hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
+                            const real *minus, real *adf_h, hipStream_t s);
 // columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
 int group_columns(int L);
 

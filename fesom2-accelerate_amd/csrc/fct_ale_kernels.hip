@@ -967,18 +967,19 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     F2A_LAUNCH_GROUPS((k_p2<1, 4>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
-hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, const real *plus, const real *minus,
-                            real *adf_h, hipStream_t s)
+hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
+                            const real *minus, real *adf_h, hipStream_t s)
 {
     const int L = nl - 1;
     int C = levels_per_thread(L);
     if (C == 2 && L % 4 == 0 && env_int("FESOM2_B3H_CPT", 2) == 4) C = 4;  // 4 levels: 2 x 16 B per array
     const int S = L / C, G = group_columns(S);
-    const long groups = (mp.n_edges + G - 1) / G;
+    const long groups = (count + G - 1) / G;
     const float invS = 1.0f / (float)S;
-    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
-    if (C == 2) F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
-    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h);
+    const int4 *ei = mp.p_edge_info + begin;
+    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
+    if (C == 2) F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
+    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
 }
 
 hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,

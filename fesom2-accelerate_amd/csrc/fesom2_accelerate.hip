@@ -279,17 +279,19 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
     if (!g_resident && (!d2h_async(bdv, st) || !d2h_async(bdh, st))) *alg_state = 0;
 }
 
-void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
-                              void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
-                              void **del_ttf_advhoriz, void **ttf, void **fct_LO, void **hnode,
-                              void **hnode_new, void **area, int *myDim_nod2D, int *eDim_nod2D,
-                              int *myDim_edge2D, int *nl, void **nlevels_nod2D,
-                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
-                              real *dt)
+// Fused phase 2 (b3h + b3v + cv + ch).  With comm/halo given, the halo exchange of fct_plus/minus
+// runs on the plan's communication stream while b3h and the node kernel process the interior
+// (no halo endpoint on any incident edge); the boundary part follows once the halo has arrived.
+static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **fct_minus, void **fct_adf_v,
+                             void **fct_adf_h, void **del_ttf_advvert, void **del_ttf_advhoriz, void **ttf,
+                             void **fct_LO, void **hnode, void **hnode_new, void **area, int *myDim_nod2D,
+                             int *eDim_nod2D, int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                             void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges, real *dt,
+                             void **comm, void **halo, const char *who)
 {
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
-    if (!check_levels(NL, "fct_ale_post_comm_c_acc_")) return;
+    if (!check_levels(NL, who)) return;
     Buffer *bplus = need(fct_plus, col_bytes(NT, L), "fct_plus"), *bminus = need(fct_minus, col_bytes(NT, L), "fct_minus");
     Buffer *bdv = need(del_ttf_advvert, col_bytes(N, L), "del_ttf_advvert");
     Buffer *bdh = need(del_ttf_advhoriz, col_bytes(N, L), "del_ttf_advhoriz");
@@ -308,14 +310,34 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
     mh.nlev_nod = bnl;
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
-    if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
-    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h_fused(plan->dev, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), st); }))
+    const f2a::MeshPlanDev &d = plan->dev;
+    if (!g_resident && !comm && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
+    hipEvent_t halo_done = nullptr;
+    if (comm) {
+        halo_done = f2a::halo_exchange_async(comm, halo, bplus, bminus, st);
+        if (!halo_done) return;
+    }
+    // with an exchange in flight only the interior goes first; otherwise everything at once
+    const int e_first = comm ? d.n_edge_interior : E, n_first = comm ? d.n_p2_interior : N;
+    f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf), dptr<real>(blo),
+                  dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
+                  dptr<real>(bdv), dptr<real>(bdh), *dt};
+    if (!run("fct_ale_b3_horizontal", st, [&] {
+            return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), st);
+        }))
         return;
-    *alg_state = 8;
-    f2a::P2Args a{NL, plan->dev.node_rec, N, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf),
-                  dptr<real>(blo), dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv),
-                  dptr<real>(badfh), dptr<real>(bdv), dptr<real>(bdh), *dt};
-    if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(plan->dev, a, st); })) return;
+    if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
+    if (comm) {
+        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
+        if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
+                return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
+                                             dptr<real>(badfh), st);
+            }))
+            return;
+        a.nodes = d.p2_rec + n_first;
+        a.count = N - n_first;
+        if (!run("fct_ale_p2_boundary", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
+    }
     *alg_state = 9;
     if (!g_resident)
         for (Buffer *b : {badfv, badfh, bdv, bdh})
@@ -323,6 +345,34 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
                 *alg_state = 0;
                 return;
             }
+}
+
+void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                              void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
+                              void **del_ttf_advhoriz, void **ttf, void **fct_LO, void **hnode,
+                              void **hnode_new, void **area, int *myDim_nod2D, int *eDim_nod2D,
+                              int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                              real *dt)
+{
+    post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
+                     fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, nullptr, nullptr, "fct_ale_post_comm_c_acc_");
+}
+
+void fct_ale_exchange_post_comm_c_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
+                                       void **fct_plus, void **fct_minus, void **fct_adf_v,
+                                       void **fct_adf_h, void **del_ttf_advvert, void **del_ttf_advhoriz,
+                                       void **ttf, void **fct_LO, void **hnode, void **hnode_new,
+                                       void **area, int *myDim_nod2D, int *eDim_nod2D,
+                                       int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                                       void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                                       real *dt)
+{
+    post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
+                     fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, comm, halo_plan,
+                     "fct_ale_exchange_post_comm_c_acc_");
 }
 
 // ----------------------------------------------------------------------------- utilities

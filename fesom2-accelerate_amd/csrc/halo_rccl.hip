@@ -33,6 +33,15 @@ struct HaloPlan {
     int *d_send = nullptr, *d_recv = nullptr;  // 0-based local columns
     real *sbuf = nullptr, *rbuf = nullptr;     // [column][plus L | minus L]
     DeviceArrays mem;
+    // communication stream + events of the overlapped exchange (created on first use)
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    ~HaloPlan()
+    {
+        if (cstream) (void)hipStreamDestroy(cstream);
+        if (ev_ready) (void)hipEventDestroy(ev_ready);
+        if (ev_done) (void)hipEventDestroy(ev_done);
+    }
 };
 
 bool nccl_ok(ncclResult_t r, const char *what)
@@ -156,33 +165,74 @@ void fesom2_halo_plan_free_(void **plan)
     *plan = nullptr;
 }
 
+}  // extern "C"
+
+// pack -> grouped send/recv -> unpack, all on stream st
+static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, hipStream_t st)
+{
+    const size_t w = 2 * (size_t)p->L;
+    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, dptr<real>(bp), dptr<real>(bm), p->sbuf, st), "halo pack"))
+        return false;
+    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return false;
+    for (size_t k = 0; k < p->ranks.size(); k++) {
+        if (p->scount[k] &&
+            !nccl_ok(ncclSend(p->sbuf + p->soff[k] * w, p->scount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclSend")) {
+            (void)ncclGroupEnd();
+            return false;
+        }
+        if (p->rcount[k] &&
+            !nccl_ok(ncclRecv(p->rbuf + p->roff[k] * w, p->rcount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclRecv")) {
+            (void)ncclGroupEnd();
+            return false;
+        }
+    }
+    if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd")) return false;
+    return ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, p->rbuf, dptr<real>(bp), dptr<real>(bm), st), "halo unpack");
+}
+
+static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm)
+{
+    const size_t need_bytes = col_bytes(p->max_col + 1, p->L);
+    for (Buffer *b : {bp, bm})
+        if (b->size < need_bytes) {
+            report("fct_plus/fct_minus holds %zu bytes, the halo plan needs %zu", b->size, need_bytes);
+            return false;
+        }
+    return true;
+}
+
+namespace f2a {
+hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm, hipStream_t s)
+{
+    Comm *c = comm_of(comm);
+    HaloPlan *p = plan_of(plan);
+    if (!c || !p || !check_buffers(p, bp, bm)) return nullptr;
+    if (!p->cstream) {
+        if (!ok(hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking), "hipStreamCreate(halo)") ||
+            !ok(hipEventCreateWithFlags(&p->ev_ready, hipEventDisableTiming), "hipEventCreate(halo)") ||
+            !ok(hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming), "hipEventCreate(halo)"))
+            return nullptr;
+    }
+    if (!ok(hipEventRecord(p->ev_ready, s), "hipEventRecord(halo ready)") ||
+        !ok(hipStreamWaitEvent(p->cstream, p->ev_ready, 0), "hipStreamWaitEvent(halo ready)"))
+        return nullptr;
+    if (!exchange_on(c, p, bp, bm, p->cstream)) return nullptr;
+    if (!ok(hipEventRecord(p->ev_done, p->cstream), "hipEventRecord(halo done)")) return nullptr;
+    return p->ev_done;
+}
+}  // namespace f2a
+
+extern "C" {
+
 void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void **fct_plus,
                            void **fct_minus)
 {
     *istat = 1;
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
-    if (!c || !p) return;
-    const size_t need_bytes = col_bytes(p->max_col + 1, p->L);
-    Buffer *bp = need(fct_plus, need_bytes, "fct_plus"), *bm = need(fct_minus, need_bytes, "fct_minus");
-    if (!bp || !bm) return;
-    const hipStream_t st = stream_of(s);
-    const size_t w = 2 * (size_t)p->L;
-    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, dptr<real>(bp), dptr<real>(bm), p->sbuf, st), "halo pack"))
-        return;
-    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return;
-    for (size_t k = 0; k < p->ranks.size(); k++) {
-        if (p->scount[k] &&
-            !nccl_ok(ncclSend(p->sbuf + p->soff[k] * w, p->scount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclSend"))
-            return;
-        if (p->rcount[k] &&
-            !nccl_ok(ncclRecv(p->rbuf + p->roff[k] * w, p->rcount[k] * w, ncclDouble, p->ranks[k], c->comm, st), "ncclRecv"))
-            return;
-    }
-    if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd")) return;
-    if (!ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, p->rbuf, dptr<real>(bp), dptr<real>(bm), st), "halo unpack"))
-        return;
-    *istat = 0;
+    Buffer *bp = buf(fct_plus, "fct_plus"), *bm = buf(fct_minus, "fct_minus");
+    if (!c || !p || !bp || !bm || !check_buffers(p, bp, bm)) return;
+    if (exchange_on(c, p, bp, bm, stream_of(s))) *istat = 0;
 }
 
 }  // extern "C"

@@ -26,7 +26,7 @@ EXPORTS = (
     "fesom2_event_record_", "fesom2_event_elapsed_", "fesom2_event_free_",
     "fesom2_kernel_timing_", "fesom2_kernel_timing_reset_", "fesom2_kernel_stats_",
     "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_halo_plan_",
-    "fesom2_halo_plan_free_", "fct_ale_exchange_acc_",
+    "fesom2_halo_plan_free_", "fct_ale_exchange_acc_", "fct_ale_exchange_post_comm_c_acc_",
 )
 
 _dll = None

@@ -169,6 +169,18 @@ void fesom2_halo_plan_free_(void **plan);
 /* Exchange fct_plus/fct_minus halo columns; enqueued on *s (work after it on *s sees the halo). */
 void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void **fct_plus,
                            void **fct_minus);
+/* Exchange + fused phase 2 with overlap: the exchange runs on the halo plan's communication stream
+ * while b3h/b3v/cv/ch process the interior (no halo endpoint), the boundary follows once the halo
+ * has arrived (docs/refactoring.md:199-235 ordering).  Same results as fct_ale_exchange_acc_ then
+ * fct_ale_post_comm_c_acc_; alg_state -> 9. */
+void fct_ale_exchange_post_comm_c_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
+                                       void **fct_plus, void **fct_minus, void **fct_adf_v,
+                                       void **fct_adf_h, void **del_ttf_advvert,
+                                       void **del_ttf_advhoriz, void **ttf, void **fct_LO,
+                                       void **hnode, void **hnode_new, void **area,
+                                       int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                       void **nlevels_nod2D, void **nlevels_elem2D,
+                                       void **nod2D_edges, void **elem2D_edges, real_type *dt);
 
 #ifdef __cplusplus
 }

@@ -114,3 +114,64 @@ def test_exchange_rejects_out_of_range_columns(comm):
 def test_plan_rejects_bad_node_numbers():
     plan, st = make_plan([0], [[0]], [[1]], 11)  # node numbers are 1-based
     assert st == 1 and not plan
+
+
+@pytest.mark.parametrize("kind", ["strips", "random"])
+def test_overlapped_exchange_post_comm_c(comm, kind):
+    """fct_ale_exchange_post_comm_c_acc_: exchange on the plan's stream, interior b3h + node kernel
+    meanwhile, boundary part after the exchange event.  Each partition's halo columns are uploaded
+    deranged (column c_j holds the true value of c_{j+1}); the one-rank plan sends c_j and receives
+    into c_{j+1}, so the halo is only right once the exchange has landed -- boundary work that ran
+    early would read wrong values.  Owned results must equal the single-domain oracle exactly."""
+    import oracle as O
+    from fesom2_amd import engine, partition, synth
+    abi.set_resident(True)
+    abi.set_path("fused")
+    nx, ny, nl, nranks = 64, 48, 21, 2
+    g = synth.make_mesh(nx, ny, nl)
+    want = O.full_pass(g, synth.make_fields(g))
+    part = (partition.strip_parts(nx, ny, nranks) if kind == "strips"
+            else np.random.default_rng(5).integers(0, nranks, g.N).astype(np.int32))
+    locs = [partition.local_mesh(g, part, r) for r in range(nranks)]
+    runs, plans, outs = [], [], []
+    try:
+        for m, _ in locs:
+            dm = engine.DeviceMesh(m)
+            runs.append((dm, engine.FctAle(dm, synth.make_fields(m))))
+        pm = []
+        for _, e in runs:
+            assert e.pre_comm() == 6
+            e.sync()
+            pm.append([e.download("plus").reshape(-1, g.L), e.download("minus").reshape(-1, g.L)])
+        for r, (m, h) in enumerate(locs):
+            for q in h.neighbors:  # the values the exchange must deliver
+                src, dst = locs[q][1].send[r] - 1, h.recv[q] - 1
+                for a in range(2):
+                    pm[r][a][dst] = pm[q][a][src]
+            cols = np.arange(m.N, m.N + m.H)
+            assert cols.size > 1
+            nxt = np.roll(cols, -1)
+            for a, name in enumerate(("plus", "minus")):
+                stored = pm[r][a].copy()
+                stored[cols] = pm[r][a][nxt]  # c_j holds the value of c_{j+1}
+                runs[r][1].upload(name, stored.reshape(-1))
+            plan, st = make_plan([0], [cols + 1], [nxt + 1], g.nl)
+            assert st == 0
+            plans.append(plan)
+        for (_, e), plan in zip(runs, plans):
+            assert e.exchange_post_comm_c(comm, plan) == 9, abi.last_error()
+        for _, e in runs:
+            e.sync()
+            outs.append({k: e.download(k) for k in ("del_v", "del_h", "adf_v", "plus")})
+    finally:
+        for plan in plans:
+            dll().fesom2_halo_plan_free_(plan.ref)
+        for dm, e in runs:
+            e.free()
+            dm.free()
+    ms = [m for m, _ in locs]
+    for r, (m, _) in enumerate(locs):  # the exchange restored the true halo
+        assert np.array_equal(outs[r]["plus"].reshape(-1, g.L)[m.N:], pm[r][0][m.N:])
+    for k in ("del_v", "del_h"):
+        assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r][k], g.L, g.N), want[k]), k
+    assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r]["adf_v"], g.nl, g.N), want["adf_v"])
