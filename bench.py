@@ -64,16 +64,22 @@ def mesh_stats(m):
     return dict(N=m.N, E=m.E, T=m.T, cn=cn, cn_halo=cn_halo, ce=ce, ring=ring)
 
 
-def kernel_bytes(s):
+def kernel_bytes(s, ntr=1):
     """Algorithmic HBM bytes per launch of each kernel of the fused pass (each array element read
-    or written once; DESIGN.md §4 derives these)."""
+    or written once; DESIGN.md §4 derives these).  ntr batched tracers: per-tracer arrays ntr
+    times, mesh fields (area_inv; area, hnode, hnode_new) and index arrays once."""
     N, E, T, cn, ch, ce, ring = s["N"], s["E"], s["T"], s["cn"], s["cn_halo"], s["ce"], s["ring"]
     cn1 = cn + N  # fct_adf_v columns carry the bottom interface too
     ints_edges = 4 * (N + 1) + 16 * 2 * E      # node->edge CSR (EdgeRef = 16 B, two per edge)
-    p1 = 8 * (2 * (cn + ch) + cn1 + cn + ce + 2 * cn) + 4 * N + ints_edges + 4 * (N + 1) + 8 * ring + 4 * N
-    b3h = 8 * (2 * ce + 2 * (cn + ch)) + 16 * E + 4 * T
-    p2 = 8 * (2 * cn + cn1 + cn + 5 * cn + 4 * cn + ce) + 4 * N + ints_edges
-    survey = 152 * cn + 24 * ce  # SURVEY.md §8(d) B_pass without ints
+    # p1: ttf, LO (owned + halo, cluster gathers), adf_v, adf_h, plus/minus written; area_inv shared
+    p1 = ntr * 8 * (2 * (cn + ch) + cn1 + ce + 2 * cn) + 8 * cn + \
+        4 * N + ints_edges + 4 * (N + 1) + 8 * ring + 4 * N
+    # b3h: adf_h read + written, plus/minus of both endpoints
+    b3h = ntr * 8 * (2 * ce + 2 * (cn + ch)) + 16 * E + 4 * T
+    # p2: plus, minus, adf_v (r + w), del_v (r + w), del_h (r + w), ttf, LO, adf_h; area, hnode,
+    # hnode_new shared
+    p2 = ntr * 8 * (9 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
+    survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "pass": p1 + b3h + p2,
             "survey_pass": survey}
 
@@ -90,18 +96,23 @@ def build_local(args, rank, world):
     return partition.local_mesh(g, part, rank)  # (local mesh, halo lists)
 
 
-def verify(args, e, step, m, f, rank, world, dist):
+def verify(args, e, step, m, fields, rank, world, dist):
     """One pass on the pristine inputs, owned results gathered on rank 0 and compared cell for cell
-    with the oracle's single-domain pass over the global mesh."""
+    with the oracle's single-domain pass over the global mesh (every tracer)."""
     for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
         e.upload(name)  # the host arrays were never touched in resident mode
     step()
     abi.device_sync()
-    L = m.L
+    L, ntr = m.L, len(fields)
+
+    def per_tracer(name, width, rows):
+        a = e.download(name).reshape(ntr, -1, width)
+        return a[:, :rows] if rows is not None else a
+
     mine = {"gid": m.node_gid[: m.N], "egid": m.edge_gid,
-            "plus": e.download("plus").reshape(-1, L)[: m.N], "minus": e.download("minus").reshape(-1, L)[: m.N],
-            "del_v": e.download("del_v").reshape(-1, L)[: m.N], "del_h": e.download("del_h").reshape(-1, L)[: m.N],
-            "adf_v": e.download("adf_v").reshape(-1, m.nl)[: m.N], "adf_h": e.download("adf_h").reshape(-1, L)}
+            "plus": per_tracer("plus", L, m.N), "minus": per_tracer("minus", L, m.N),
+            "del_v": per_tracer("del_v", L, m.N), "del_h": per_tracer("del_h", L, m.N),
+            "adf_v": per_tracer("adf_v", m.nl, m.N), "adf_h": per_tracer("adf_h", L, None)}
     if dist is not None:
         parts = [None] * world
         dist.all_gather_object(parts, mine)
@@ -113,24 +124,26 @@ def verify(args, e, step, m, f, rank, world, dist):
     import oracle as O
     nx, ny, nl = synth.CONFIGS[args.config]
     g = synth.make_mesh(nx, ny * world, nl, full_depth=not args.parity_levels)
-    want = O.full_pass(g, synth.make_fields(g))
     wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
     bad = {}
-    for p in parts:
-        gid = p["gid"]
-        for k in ("plus", "minus"):
-            w = want[k].reshape(-1, L)[gid]
-            n = int(np.sum((p[k] != w) & wet[gid]))
+    for k, fk in enumerate(synth.make_tracer_fields(g, ntr)):
+        want = O.full_pass(g, fk)
+        for p in parts:
+            gid = p["gid"]
+            for name in ("plus", "minus"):
+                w = want[name].reshape(-1, L)[gid]
+                n = int(np.sum((p[name][k] != w) & wet[gid]))
+                if n:
+                    bad[name] = bad.get(name, 0) + n
+            for name, stride in (("del_v", L), ("del_h", L), ("adf_v", nl)):
+                n = int(np.sum(p[name][k] != want[name].reshape(-1, stride)[gid]))
+                if n:
+                    bad[name] = bad.get(name, 0) + n
+            n = int(np.sum(p["adf_h"][k] != want["adf_h"].reshape(-1, L)[p["egid"]]))
             if n:
-                bad[k] = bad.get(k, 0) + n
-        for k, stride in (("del_v", L), ("del_h", L), ("adf_v", nl)):
-            n = int(np.sum(p[k] != want[k].reshape(-1, stride)[gid]))
-            if n:
-                bad[k] = bad.get(k, 0) + n
-        n = int(np.sum(p["adf_h"] != want["adf_h"].reshape(-1, L)[p["egid"]]))
-        if n:
-            bad["adf_h"] = bad.get("adf_h", 0) + n
-    return {"exact": not bad, "mismatched_cells": bad, "against": "oracle full pass on the global mesh"}
+                bad["adf_h"] = bad.get("adf_h", 0) + n
+    return {"exact": not bad, "mismatched_cells": bad, "tracers": ntr,
+            "against": "oracle full pass on the global mesh, per tracer"}
 
 
 def main():
@@ -143,6 +156,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
     ap.add_argument("--path", default="fused", choices=["fused", "stepwise"])
+    ap.add_argument("--tracers", type=int, default=1,
+                    help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
                          "oracle on the global mesh (gathered over ranks)")
@@ -167,12 +182,15 @@ def main():
 
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
-    f = synth.make_fields(m)
+    if args.tracers > 1 and args.path != "fused":
+        raise SystemExit("--tracers > 1 runs the batched (fused) entry points only")
+    fields = synth.make_tracer_fields(m, args.tracers)
+    f = fields[0]
     abi.set_resident(True)
     abi.set_path(args.path)
     dm = engine.DeviceMesh(m)
     dm.prepare()
-    e = engine.FctAle(dm, f)
+    e = engine.FctAle(dm, f) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
     stream = e.stream
 
     halo = None
@@ -241,11 +259,11 @@ def main():
         total_cells = float(mesh_stats(m)["cn"])
 
     ms_step = 1e3 * wall / args.steps
-    value = total_cells / (wall / args.steps)
+    value = args.tracers * total_cells / (wall / args.steps)  # tracer cell-updates
 
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
     s = mesh_stats(m)
-    kb = kernel_bytes(s)
+    kb = kernel_bytes(s, args.tracers)
     per_kernel = {}
     for name, (cnt, tot) in stats.items():
         avg = tot / max(cnt, 1)
@@ -259,7 +277,8 @@ def main():
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
-        if tr.get("workload") == args.config and dom in tr.get("bytes_per_launch", {}):
+        if tr.get("workload") == args.config and tr.get("tracers", 1) == args.tracers and \
+                dom in tr.get("bytes_per_launch", {}):
             traffic = tr["bytes_per_launch"][dom]
     except (OSError, ValueError):
         pass
@@ -284,7 +303,7 @@ def main():
 
     check = None
     if args.check:
-        check = verify(args, e, step, m, f, rank, world, dist)
+        check = verify(args, e, step, m, fields, rank, world, dist)
 
     if rank == 0:
         out = {
@@ -292,8 +311,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
-            "config": {"workload": f"{args.config} full-depth, 1 tracer per GPU" if not args.parity_levels
-                       else f"{args.config} parity levels, 1 tracer per GPU",
+            "config": {"workload": f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}, "
+                                   f"{args.tracers} tracer{'s' if args.tracers > 1 else ''} per GPU"
+                                   + (" (batched)" if args.tracers > 1 else ""),
+                       "tracers": args.tracers,
                        "nodes_per_gpu": m.N, "levels": m.L, "global_nodes": m.N * world if world > 1 else m.N,
                        "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
                        "parallelism": f"node partition y-strips x{world}, RCCL halo" if world > 1 else "1 GPU",
@@ -302,7 +323,7 @@ def main():
             "cpu_baseline": cpu,
             "pass_roofline": {"alg_bytes": kb["survey_pass"], "GBps": round(pass_gbs, 1),
                               "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
-                              "note": "SURVEY.md 8(d) B_pass = 152 Cn + 24 Ce over the whole pass"},
+                              "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
             "kernels": per_kernel,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "setup_s": round(setup_s, 1),

@@ -102,6 +102,8 @@ void drop_plans_of(const Buffer *b);
 // ---- halo exchange (halo_rccl.hip): enqueue pack -> grouped ncclSend/ncclRecv -> unpack on the
 // halo plan's communication stream after the work already queued on `s`.  Returns an event that
 // completes when the halo columns hold the neighbours' values (nullptr on failure).
-hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *plus, Buffer *minus, hipStream_t s);
+// ntr tracers of plus/minus, `stride` doubles apart (the batched layouts)
+hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *plus, Buffer *minus, int ntr, size_t stride,
+                               hipStream_t s);
 
 }  // namespace f2a

@@ -89,9 +89,16 @@ struct MeshPlanDev {
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
     int n_p2_interior = 0;
-    // local edges with no owned endpoint (b3-horizontal still applies to them)
-    const int *orphan_edges = nullptr;
-    int n_orphans = 0;
+};
+
+// Batched tracers: `n` tracers whose per-tracer arrays follow each other in one buffer, `node`
+// elements apart for (L, nodes) fields, `lev` apart for (nl, nodes) fields (fct_adf_v), `edge` apart
+// for fct_adf_h.  Mesh-only fields (area, area_inv, hnode, hnode_new) are shared.  Block tiles map
+// to (column group, tracer) with the tracer fastest, so the n blocks of one column group run back to
+// back on one XCD and share its L2 for the records and the shared fields.
+struct Tracers {
+    int n = 1;
+    size_t node = 0, lev = 0, edge = 0;
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().
@@ -101,6 +108,7 @@ struct P1Args {
     const real *ttf, *LO, *adf_v, *adf_h, *area_inv;
     real *plus, *minus;
     real dt, eps, big;
+    Tracers tr;
 };
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 
@@ -111,11 +119,12 @@ struct P2Args {
     const real *plus, *minus, *ttf, *LO, *hnode, *hnode_new, *area;
     real *adf_v, *adf_h, *del_v, *del_h;
     real dt;
+    Tracers tr;
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
-                            const real *minus, real *adf_h, hipStream_t s);
+                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
 // columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
 int group_columns(int L);
 
@@ -148,10 +157,11 @@ hipError_t launch_cv(int n_owned, int nl, const int *nlev_nod, const real *ttf, 
 hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const real *area,
                      real *del_h, real dt, hipStream_t s);
 
-// Halo pack / unpack of (plus, minus) columns.
-hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,
+// Halo pack / unpack of (plus, minus) columns of ntr tracers (`stride` elements apart); the buffer
+// holds [list position][tracer][plus L | minus L], so each neighbour's part stays contiguous.
+hipError_t launch_halo_pack(const int *nodes, int count, int L, int ntr, size_t stride, const real *plus,
                             const real *minus, real *buf, hipStream_t s);
-hipError_t launch_halo_unpack(const int *nodes, int count, int L, const real *buf, real *plus,
-                              real *minus, hipStream_t s);
+hipError_t launch_halo_unpack(const int *nodes, int count, int L, int ntr, size_t stride, const real *buf,
+                              real *plus, real *minus, hipStream_t s);
 
 }  // namespace f2a

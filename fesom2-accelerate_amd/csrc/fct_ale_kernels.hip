@@ -39,6 +39,8 @@ __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements)
 // FESOM2_ABLATE (timing-only builds of an experiment, results are wrong): bit 0 skips the cluster
 // gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2.
 __constant__ int c_ablate = 0;
+// FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile order
+__constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
 {
@@ -56,6 +58,11 @@ static void init_swizzle()
     if (e && atoi(e) == 0) {
         const int zero = 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_xcd_swizzle), &zero, sizeof zero);
+    }
+    const char *tm = getenv("FESOM2_TRACER_MAJOR");
+    if (tm) {
+        const int v = atoi(tm);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_major), &v, sizeof v);
     }
     const char *ab = getenv("FESOM2_ABLATE");
     if (ab && atoi(ab)) {
@@ -414,6 +421,27 @@ __device__ __forceinline__ void slot_of(int t, int S, float invS, int &j, int &u
 
 __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
 
+// tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
+// for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
+// keep the L2 to themselves)
+__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false)
+{
+    const int t = block_tile();
+    if (ntr == 1) {
+        tr = 0;
+        return t;
+    }
+    if (major) {
+        const int groups = gridDim.x / ntr;
+        tr = t / groups;
+        return t - tr * groups;
+    }
+    const int g = t / ntr;
+    tr = t - g * ntr;
+    return g;
+}
+
+
 // C consecutive levels; C even reads 16-byte pairs (p 16-byte aligned)
 template <int C>
 __device__ __forceinline__ void ldv(const real *__restrict__ p, real (&v)[C])
@@ -445,6 +473,56 @@ __device__ __forceinline__ void stv(real *__restrict__ p, const real (&v)[C], in
                 p[c] = v[c];
         }
     }
+}
+
+// Single-use streams (a column nobody else reads in the same kernel) can bypass the L2 with
+// non-temporal loads/stores, leaving it to the gathered columns.
+typedef double f2a_d2 __attribute__((ext_vector_type(2)));
+template <int C, bool NT>
+__device__ __forceinline__ void ldv_s(const real *__restrict__ p, real (&v)[C])
+{
+    if constexpr (NT && C % 2 == 0) {
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+            const f2a_d2 t = __builtin_nontemporal_load(reinterpret_cast<const f2a_d2 *>(p + c));
+            v[c] = t.x;
+            v[c + 1] = t.y;
+        }
+    } else {
+        ldv<C>(p, v);
+    }
+}
+template <int C, bool NT>
+__device__ __forceinline__ void stv_s(real *__restrict__ p, const real (&v)[C], int n)
+{
+    if constexpr (NT && C % 2 == 0) {
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+            if (c + 2 <= n) {
+                f2a_d2 t;
+                t.x = v[c];
+                t.y = v[c + 1];
+                __builtin_nontemporal_store(t, reinterpret_cast<f2a_d2 *>(p + c));
+            } else if (c < n) {
+                p[c] = v[c];
+            }
+        }
+    } else {
+        stv<C>(p, v, n);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ real ld1_s(const real *__restrict__ p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st1_s(real *__restrict__ p, real v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 // tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
@@ -537,13 +615,22 @@ __device__ __forceinline__ const NodeRec *stage_records(const NodeRec *__restric
     return r;
 }
 
-template <int VLIMIT, int C, int RB, int EB>
+template <int VLIMIT, int C, int RB, int EB, bool NT>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
     const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
-    const int first = block_tile() * G;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 1) * G;
+    if (tr) {
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
     const int ncol = min(G, a.n_owned - first);
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     int j, u;
@@ -563,7 +650,7 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         ab = (size_t)ni.n * a.nl + z0;
         real v[C + 1];
 #pragma unroll
-        for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? a.adf_v[ab + c] : 0.;
+        for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? ld1_s<NT>(a.adf_v + ab + c) : 0.;
 #pragma unroll
         for (int c = 0; c < C; c++) {
             p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
@@ -605,7 +692,7 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     real lo[C], ai[C], op[C], om[C];
     ldv<C>(a.LO + b, lo);
 #pragma unroll
-    for (int c = 0; c < C; c++) ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
+    for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
 #pragma unroll
     for (int c = 0; c < C; c++) {
         op[c] = om[c] = 0.;
@@ -644,8 +731,8 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         flux = m[c] * a.dt * ai[c] - a.eps;
         om[c] = RMIN(1., (tn - lo[c]) / flux);
     }
-    stv<C>(a.plus + b, op, nw);
-    stv<C>(a.minus + b, om, nw);
+    stv_s<C, NT>(a.plus + b, op, nw);
+    stv_s<C, NT>(a.minus + b, om, nw);
 }
 
 // Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
@@ -653,12 +740,15 @@ template <int C>
 __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, int n_edges, int L,
                                                 int G, float invS, const real *__restrict__ plus,
                                                 const real *__restrict__ minus,
-                                                real *__restrict__ adf_h)
+                                                real *__restrict__ adf_h, Tracers trs)
 {
-    int j, u;
+    int j, u, tr;
     slot_of(threadIdx.x, L / C, invS, j, u);
     const int z0 = C * u;
-    const int k = block_tile() * G + j;
+    const int k = group_tracer(trs.n, tr, c_tracer_major & 2) * G + j;
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
     if (j >= G || k >= n_edges) return;
     const int4 ei = einfo[k];  // {node1, node2, lev, edge}
     const int nw = min(C, ei.z - z0);
@@ -676,18 +766,76 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
     stv<C>(adf_h + i, out, nw);
 }
 
+// Same, U consecutive edge groups per block: every einfo load of the U groups is issued, then every
+// data load, so a thread keeps U x 5 loads in flight instead of 5 (memory-level parallelism), and
+// the grid has U times fewer blocks.  NT: fct_adf_h streamed with non-temporal loads/stores so the
+// gathered plus/minus columns keep the L2.
+template <int C, int U, bool NT>
+__global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, int n_edges, int L,
+                                                int G, float invS, const real *__restrict__ plus,
+                                                const real *__restrict__ minus,
+                                                real *__restrict__ adf_h, Tracers trs)
+{
+    int j, u, tr;
+    slot_of(threadIdx.x, L / C, invS, j, u);
+    if (j >= G) return;
+    const int z0 = C * u;
+    const int k0 = group_tracer(trs.n, tr, c_tracer_major & 2) * U * G + j;
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
+    int4 ei[U];
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+        const int k = k0 + q * G;
+        ei[q] = k < n_edges ? einfo[k] : make_int4(0, 0, 0, 0);
+    }
+    real f[U][C], p1[U][C], m1[U][C], p2[U][C], m2[U][C];
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+        if (z0 < ei[q].z) {
+            ldv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, f[q]);
+            const size_t i1 = (size_t)ei[q].x * L + z0, i2 = (size_t)ei[q].y * L + z0;
+            ldv<C>(plus + i1, p1[q]);
+            ldv<C>(minus + i1, m1[q]);
+            ldv<C>(plus + i2, p2[q]);
+            ldv<C>(minus + i2, m2[q]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+        const int nw = min(C, ei[q].z - z0);
+        if (nw <= 0) continue;
+        real out[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) out[c] = b3h_factor(f[q][c], p1[q][c], m1[q][c], p2[q][c], m2[q][c]) * f[q][c];
+        stv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, out, nw);
+    }
+}
+
 // Phase 2, nodes: b3v + cv + ch, G node columns per block.  fct_adf_h already holds the b3-limited
 // fluxes (k_b3h_g ran first, as in docs/refactoring.md:237-314).  The limited vertical flux of the
 // interface below a thread's levels is recomputed in-thread from plus/minus (the bottom interface
 // nlev-1 is never limited); the barrier orders every raw fct_adf_v read of the block before its
 // writes.
-template <int C, int KB>
+template <int C, int KB, bool NT>
 __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
-    const int first = block_tile() * G;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.del_v += tr * a.tr.node;
+        a.del_h += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
     const int ncol = min(G, a.count - first);
     const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
     int j, u;
@@ -711,8 +859,8 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
         mm[0] = z0 ? a.minus[b - 1] : 0.;
         {
             real tp[C], tmn[C];
-            ldv<C>(a.plus + b, tp);
-            ldv<C>(a.minus + b, tmn);
+            ldv_s<C, NT>(a.plus + b, tp);
+            ldv_s<C, NT>(a.minus + b, tmn);
 #pragma unroll
             for (int c = 0; c < C; c++) {
                 pp[c + 1] = tp[c];
@@ -735,16 +883,16 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
         for (int c = 0; c < C; c++) l[c] = lim[c];
         if (nw > 0) {
             real del_v[C], ttf[C], hn[C], lo[C], hnn[C];
-            ldv<C>(a.del_v + b, del_v);
-            ldv<C>(a.ttf + b, ttf);
-            ldv<C>(a.hnode + b, hn);
-            ldv<C>(a.LO + b, lo);
-            ldv<C>(a.hnode_new + b, hnn);
-            ldv<C>(a.del_h + b, dh);
+            ldv_s<C, NT>(a.del_v + b, del_v);
+            ldv_s<C, NT>(a.ttf + b, ttf);
+            ldv_s<C, NT>(a.hnode + b, hn);
+            ldv_s<C, NT>(a.LO + b, lo);
+            ldv_s<C, NT>(a.hnode_new + b, hnn);
+            ldv_s<C, NT>(a.del_h + b, dh);
             real dta[C];
 #pragma unroll
             for (int c = 0; c < C; c++) {
-                dta[c] = c < nw ? a.dt / a.area[ab + c] : 0.;
+                dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
                 real tv = del_v[c] - ttf[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
                 tv = tv + lo[c] * hnn[c];
                 dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
@@ -761,10 +909,10 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     if (na <= 0) return;
 #pragma unroll
     for (int c = 0; c < C; c++)
-        if (c < na) a.adf_v[ab + c] = l[c];
+        if (c < na) st1_s<NT>(a.adf_v + ab + c, l[c]);
     if (nw <= 0) return;
-    stv<C>(a.del_v + b, dv, nw);
-    stv<C>(a.del_h + b, dh, nw);
+    stv_s<C, NT>(a.del_v + b, dv, nw);
+    stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
 // columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads)
@@ -796,13 +944,15 @@ static inline int levels_per_thread(int L)
 // ============================================================================ halo pack / unpack
 
 __global__ __launch_bounds__(kBlock) void k_pack(const int *__restrict__ nodes, int count, int L,
+                                                 int ntr, size_t stride,
                                                  const real *__restrict__ plus,
                                                  const real *__restrict__ minus,
                                                  real *__restrict__ buf)
 {
-    const int i = wave_item();
-    if (i >= count) return;
-    const size_t src = (size_t)nodes[i] * L, dst = (size_t)i * 2 * L;
+    const int i = wave_item();  // list position * ntr + tracer
+    if (i >= count * ntr) return;
+    const int c = i / ntr, tr = i - c * ntr;
+    const size_t src = tr * stride + (size_t)nodes[c] * L, dst = (size_t)i * 2 * L;
     for (int z = threadIdx.x & 63; z < L; z += kWave) {
         buf[dst + z] = plus[src + z];
         buf[dst + L + z] = minus[src + z];
@@ -810,13 +960,15 @@ __global__ __launch_bounds__(kBlock) void k_pack(const int *__restrict__ nodes, 
 }
 
 __global__ __launch_bounds__(kBlock) void k_unpack(const int *__restrict__ nodes, int count, int L,
+                                                   int ntr, size_t stride,
                                                    const real *__restrict__ buf,
                                                    real *__restrict__ plus,
                                                    real *__restrict__ minus)
 {
     const int i = wave_item();
-    if (i >= count) return;
-    const size_t dst = (size_t)nodes[i] * L, src = (size_t)i * 2 * L;
+    if (i >= count * ntr) return;
+    const int c = i / ntr, tr = i - c * ntr;
+    const size_t dst = tr * stride + (size_t)nodes[c] * L, src = (size_t)i * 2 * L;
     for (int z = threadIdx.x & 63; z < L; z += kWave) {
         plus[dst + z] = buf[src + z];
         minus[dst + z] = buf[src + L + z];
@@ -933,15 +1085,17 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
 {
     const float invS = 1.0f / (float)S;
     const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real) + (size_t)G * sizeof(NodeRec);
-    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
-    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB>), groups, G, S, lds, s, mp, a, G, invS);
+    const bool NT = (env_int("FESOM2_NT", 0) & 1) != 0;
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
+    if (NT) F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
-    const long groups = (a.n_owned + G - 1) / G;
+    const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     // batch sizes of the cluster / edge gathers (FESOM2_P1_BATCH = 10*RB + EB; measured)
     switch (env_int("FESOM2_P1_BATCH", 22)) {
     case 44: return C == 2 ? p1_launch<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch<1, 4, 4>(mp, a, s, G, S, groups);
@@ -955,20 +1109,22 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
-    const long groups = (a.count + G - 1) / G;
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const int KB = env_int("FESOM2_P2_BATCH", 4);
     const size_t lds = (size_t)G * sizeof(NodeRec);
     if (C == 2) {
-        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2<2, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        const bool NT = (env_int("FESOM2_NT", 0) & 2) != 0;
+        if (NT) F2A_LAUNCH_GROUPS((k_p2<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8>), groups, G, S, lds, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p2<1, 4>), groups, G, S, lds, s, mp, a, G, invS);
+    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
-                            const real *minus, real *adf_h, hipStream_t s)
+                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
     const int L = nl - 1;
     int C = levels_per_thread(L);
@@ -977,21 +1133,38 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
     const long groups = (count + G - 1) / G;
     const float invS = 1.0f / (float)S;
     const int4 *ei = mp.p_edge_info + begin;
-    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
-    if (C == 2) F2A_LAUNCH_GROUPS(k_b3h_g<2>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
-    F2A_LAUNCH_GROUPS(k_b3h_g<1>, groups, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h);
+    const long tg = groups * tr.n;
+    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+    if (C == 2) {
+        // U edge groups per block, fct_adf_h non-temporal (FESOM2_B3H_U / FESOM2_B3H_NT; measured)
+        const int U = env_int("FESOM2_B3H_U", 2);
+        const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
+        const long ug = (groups + U - 1) / U * tr.n;
+#define F2A_B3H_U(UU)                                                                                   \
+        if (U == UU) {                                                                                  \
+            if (NT) F2A_LAUNCH_GROUPS((k_b3h_u<2, UU, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr); \
+            F2A_LAUNCH_GROUPS((k_b3h_u<2, UU, false>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr); \
+        }
+        F2A_B3H_U(2)
+        F2A_B3H_U(4)
+        F2A_B3H_U(8)
+#undef F2A_B3H_U
+        if (NT) F2A_LAUNCH_GROUPS((k_b3h_u<2, 1, true>), tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+    }
+    F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
 }
 
-hipError_t launch_halo_pack(const int *nodes, int count, int L, const real *plus,
+hipError_t launch_halo_pack(const int *nodes, int count, int L, int ntr, size_t stride, const real *plus,
                             const real *minus, real *buf, hipStream_t s)
 {
-    F2A_LAUNCH(k_pack, count, 0, s, nodes, count, L, plus, minus, buf);
+    F2A_LAUNCH(k_pack, (long)count * ntr, 0, s, nodes, count, L, ntr, stride, plus, minus, buf);
 }
 
-hipError_t launch_halo_unpack(const int *nodes, int count, int L, const real *buf, real *plus,
-                              real *minus, hipStream_t s)
+hipError_t launch_halo_unpack(const int *nodes, int count, int L, int ntr, size_t stride, const real *buf,
+                              real *plus, real *minus, hipStream_t s)
 {
-    F2A_LAUNCH(k_unpack, count, 0, s, nodes, count, L, buf, plus, minus);
+    F2A_LAUNCH(k_unpack, (long)count * ntr, 0, s, nodes, count, L, ntr, stride, buf, plus, minus);
 }
 
 }  // namespace f2a

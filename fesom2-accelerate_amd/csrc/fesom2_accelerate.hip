@@ -197,6 +197,61 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
     finish(6, {bplus, bminus});
 }
 
+// Batched phase 1 (a1..b2, fused) of ntracers tracers in one launch: per-tracer handles hold the
+// tracers one after another, (N+H)*L doubles apart (ttf, fct_LO, fct_plus, fct_minus), (N+H)*nl
+// apart (fct_adf_v) and E*L apart (fct_adf_h); area_inv is shared.  alg_state 6 on success.
+void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                   void **fct_minus, void **ttf, void **fct_LO, void **fct_adf_v,
+                                   void **fct_adf_h, void **area_inv, int *myDim_nod2D,
+                                   int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                                   void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                                   void **nod_in_elem2D_num, void **nod_in_elem2D,
+                                   int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges,
+                                   int *vlimit, real *flux_eps, real *bignumber, real *dt)
+{
+    *alg_state = 0;
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = *myDim_nod2D + *eDim_nod2D, T = *myDim_elem2D, E = *myDim_edge2D;
+    const int NL = *nl, L = NL - 1, ntr = *ntracers;
+    if (!check_levels(NL, "fct_ale_pre_comm_batched_acc_")) return;
+    if (ntr < 1) {
+        report("fct_ale_pre_comm_batched_acc_: ntracers = %d", ntr);
+        return;
+    }
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = need(nlevels_elem2D, sizeof(int) * (size_t)T, "nlevels_elem2D");
+    Buffer *bnlnod = need(nlevels_nod2D, sizeof(int) * (size_t)NT, "nlevels_nod2D");
+    mh.elem_nodes = need(elem2D_nodes, 3 * sizeof(int) * (size_t)T, "elem2D_nodes");
+    mh.nie = buf(nod_in_elem2D, "nod_in_elem2D");
+    mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
+    mh.dim = *nod_in_elem2D_dim;
+    const size_t nodeb = col_bytes(NT, L) * ntr;
+    Buffer *bplus = need(fct_plus, nodeb, "fct_plus"), *bminus = need(fct_minus, nodeb, "fct_minus");
+    Buffer *bttf = need(ttf, nodeb, "ttf"), *blo = need(fct_LO, nodeb, "fct_LO");
+    Buffer *badfv = need(fct_adf_v, col_bytes(NT, NL) * ntr, "fct_adf_v");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L) * ntr, "fct_adf_h");
+    Buffer *bainv = need(area_inv, col_bytes(N, NL), "area_inv");
+    if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie || !mh.nie_num ||
+        !bplus || !bminus || !bttf || !blo || !badfv || !badfh || !bainv)
+        return;
+    mh.nlev_nod = bnlnod;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, true);
+    if (!plan) return;
+    if (!g_resident && !h2d(blo, false, st, false)) return;
+    wait_event(bttf, st);
+    wait_event(badfv, st);
+    wait_event(badfh, st);
+    f2a::P1Args a{N, NL, *vlimit, dptr<int>(bnlnod), dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
+                  dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
+                  *dt, *flux_eps, *bignumber};
+    a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) return;
+    *alg_state = 6;
+    if (!g_resident && (!d2h_async(bplus, st) || !d2h_async(bminus, st))) *alg_state = 0;
+}
+
 // ----------------------------------------------------------------------------- phase 2
 
 void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
@@ -287,17 +342,25 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                              void **fct_LO, void **hnode, void **hnode_new, void **area, int *myDim_nod2D,
                              int *eDim_nod2D, int *myDim_edge2D, int *nl, void **nlevels_nod2D,
                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges, real *dt,
-                             void **comm, void **halo, const char *who)
+                             void **comm, void **halo, int ntr, const char *who)
 {
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
     if (!check_levels(NL, who)) return;
-    Buffer *bplus = need(fct_plus, col_bytes(NT, L), "fct_plus"), *bminus = need(fct_minus, col_bytes(NT, L), "fct_minus");
-    Buffer *bdv = need(del_ttf_advvert, col_bytes(N, L), "del_ttf_advvert");
-    Buffer *bdh = need(del_ttf_advhoriz, col_bytes(N, L), "del_ttf_advhoriz");
-    Buffer *bttf = need(ttf, col_bytes(N, L), "ttf"), *blo = need(fct_LO, col_bytes(N, L), "fct_LO");
+    if (ntr < 1) {
+        report("%s: ntracers = %d", who, ntr);
+        return;
+    }
+    // one tracer: the reference's sizes; batched: (N+H)-column blocks per tracer (see pre_comm)
+    const bool batched = ntr > 1;
+    const size_t own = batched ? col_bytes(NT, L) * ntr : col_bytes(N, L);
+    Buffer *bplus = need(fct_plus, col_bytes(NT, L) * ntr, "fct_plus"), *bminus = need(fct_minus, col_bytes(NT, L) * ntr, "fct_minus");
+    Buffer *bdv = need(del_ttf_advvert, own, "del_ttf_advvert");
+    Buffer *bdh = need(del_ttf_advhoriz, own, "del_ttf_advhoriz");
+    Buffer *bttf = need(ttf, own, "ttf"), *blo = need(fct_LO, own, "fct_LO");
     Buffer *bh = need(hnode, col_bytes(N, L), "hnode"), *bhn = need(hnode_new, col_bytes(N, L), "hnode_new");
-    Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v"), *badfh = need(fct_adf_h, col_bytes(E, L), "fct_adf_h");
+    Buffer *badfv = need(fct_adf_v, batched ? col_bytes(NT, NL) * ntr : col_bytes(N, NL), "fct_adf_v");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L) * ntr, "fct_adf_h");
     Buffer *barea = need(area, col_bytes(N, NL), "area");
     Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
     MeshHandles mh;
@@ -314,7 +377,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
     if (!g_resident && !comm && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
     hipEvent_t halo_done = nullptr;
     if (comm) {
-        halo_done = f2a::halo_exchange_async(comm, halo, bplus, bminus, st);
+        halo_done = f2a::halo_exchange_async(comm, halo, bplus, bminus, ntr, (size_t)NT * L, st);
         if (!halo_done) return;
     }
     // with an exchange in flight only the interior goes first; otherwise everything at once
@@ -322,8 +385,9 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
     f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bttf), dptr<real>(blo),
                   dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
+    a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
     if (!run("fct_ale_b3_horizontal", st, [&] {
-            return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), st);
+            return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
         }))
         return;
     if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
@@ -331,7 +395,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
         if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
                 return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
-                                             dptr<real>(badfh), st);
+                                             dptr<real>(badfh), a.tr, st);
             }))
             return;
         a.nodes = d.p2_rec + n_first;
@@ -357,7 +421,7 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
 {
     post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
                      fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
-                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, nullptr, nullptr, "fct_ale_post_comm_c_acc_");
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, nullptr, nullptr, 1, "fct_ale_post_comm_c_acc_");
 }
 
 void fct_ale_exchange_post_comm_c_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
@@ -371,8 +435,39 @@ void fct_ale_exchange_post_comm_c_acc_(int *alg_state, void **s, void **comm, vo
 {
     post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
                      fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
-                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, comm, halo_plan,
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, comm, halo_plan, 1,
                      "fct_ale_exchange_post_comm_c_acc_");
+}
+
+// Batched fused phase 2 (layouts as fct_ale_pre_comm_batched_acc_; hnode, hnode_new, area shared).
+void fct_ale_post_comm_c_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                      void **fct_minus, void **fct_adf_v, void **fct_adf_h,
+                                      void **del_ttf_advvert, void **del_ttf_advhoriz, void **ttf,
+                                      void **fct_LO, void **hnode, void **hnode_new, void **area,
+                                      int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                      void **nlevels_nod2D, void **nlevels_elem2D,
+                                      void **nod2D_edges, void **elem2D_edges, real *dt)
+{
+    post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
+                     fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, nullptr, nullptr, *ntracers,
+                     "fct_ale_post_comm_c_batched_acc_");
+}
+
+// Batched, with the halo exchange of all tracers overlapped with the interior.
+void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
+                                               int *ntracers, void **fct_plus, void **fct_minus,
+                                               void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
+                                               void **del_ttf_advhoriz, void **ttf, void **fct_LO,
+                                               void **hnode, void **hnode_new, void **area,
+                                               int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D,
+                                               int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                                               void **nod2D_edges, void **elem2D_edges, real *dt)
+{
+    post_comm_c_impl(alg_state, s, fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert, del_ttf_advhoriz, ttf,
+                     fct_LO, hnode, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
+                     nlevels_elem2D, nod2D_edges, elem2D_edges, dt, comm, halo_plan, *ntracers,
+                     "fct_ale_exchange_post_comm_c_batched_acc_");
 }
 
 // ----------------------------------------------------------------------------- utilities

@@ -31,7 +31,8 @@ struct HaloPlan {
     std::vector<int> ranks, scount, rcount, soff, roff;  // offsets in columns
     int nsend = 0, nrecv = 0, max_col = -1;
     int *d_send = nullptr, *d_recv = nullptr;  // 0-based local columns
-    real *sbuf = nullptr, *rbuf = nullptr;     // [column][plus L | minus L]
+    real *sbuf = nullptr, *rbuf = nullptr;     // [list position][tracer][plus L | minus L]
+    int buf_tracers = 0;                       // tracers the buffers hold
     DeviceArrays mem;
     // communication stream + events of the overlapped exchange (created on first use)
     hipStream_t cstream = nullptr;
@@ -67,6 +68,19 @@ HaloPlan *plan_of(void **h)
         return nullptr;
     }
     return static_cast<HaloPlan *>(*h);
+}
+
+// pack/recv buffers for ntr tracers (grown on first use by a larger batch; the old ones stay in
+// the plan's arena until it is freed)
+bool reserve_tracers(HaloPlan *p, int ntr)
+{
+    if (ntr <= p->buf_tracers) return true;
+    const size_t w = sizeof(real) * 2 * (size_t)p->L * ntr;
+    p->sbuf = static_cast<real *>(p->mem.alloc(w * std::max(p->nsend, 1)));
+    p->rbuf = static_cast<real *>(p->mem.alloc(w * std::max(p->nrecv, 1)));
+    if (!p->sbuf || !p->rbuf) return false;
+    p->buf_tracers = ntr;
+    return true;
 }
 
 }  // namespace
@@ -146,9 +160,7 @@ void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_cou
     }
     p->d_send = p->mem.upload(snodes);
     p->d_recv = p->mem.upload(rnodes);
-    p->sbuf = static_cast<real *>(p->mem.alloc(sizeof(real) * 2 * (size_t)p->L * std::max(p->nsend, 1)));
-    p->rbuf = static_cast<real *>(p->mem.alloc(sizeof(real) * 2 * (size_t)p->L * std::max(p->nrecv, 1)));
-    if (!p->d_send || !p->d_recv || !p->sbuf || !p->rbuf) {
+    if (!p->d_send || !p->d_recv || !reserve_tracers(p, 1)) {
         delete p;
         return;
     }
@@ -167,11 +179,13 @@ void fesom2_halo_plan_free_(void **plan)
 
 }  // extern "C"
 
-// pack -> grouped send/recv -> unpack, all on stream st
-static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, hipStream_t st)
+// pack -> grouped send/recv -> unpack, all on stream st (ntr tracers, `stride` doubles apart)
+static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t stride, hipStream_t st)
 {
-    const size_t w = 2 * (size_t)p->L;
-    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, dptr<real>(bp), dptr<real>(bm), p->sbuf, st), "halo pack"))
+    if (!reserve_tracers(p, ntr)) return false;
+    const size_t w = 2 * (size_t)p->L * ntr;  // doubles per list position
+    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, ntr, stride, dptr<real>(bp), dptr<real>(bm), p->sbuf, st),
+            "halo pack"))
         return false;
     if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return false;
     for (size_t k = 0; k < p->ranks.size(); k++) {
@@ -187,12 +201,17 @@ static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, hipStream_
         }
     }
     if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd")) return false;
-    return ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, p->rbuf, dptr<real>(bp), dptr<real>(bm), st), "halo unpack");
+    return ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, ntr, stride, p->rbuf, dptr<real>(bp), dptr<real>(bm), st),
+              "halo unpack");
 }
 
-static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm)
+static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t stride)
 {
-    const size_t need_bytes = col_bytes(p->max_col + 1, p->L);
+    if (ntr < 1 || (ntr > 1 && stride < (size_t)(p->max_col + 1) * p->L)) {
+        report("halo exchange: %d tracers %zu doubles apart do not fit columns up to %d", ntr, stride, p->max_col + 1);
+        return false;
+    }
+    const size_t need_bytes = sizeof(real) * (stride * (ntr - 1)) + col_bytes(p->max_col + 1, p->L);
     for (Buffer *b : {bp, bm})
         if (b->size < need_bytes) {
             report("fct_plus/fct_minus holds %zu bytes, the halo plan needs %zu", b->size, need_bytes);
@@ -202,11 +221,11 @@ static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm)
 }
 
 namespace f2a {
-hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm, hipStream_t s)
+hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm, int ntr, size_t stride, hipStream_t s)
 {
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
-    if (!c || !p || !check_buffers(p, bp, bm)) return nullptr;
+    if (!c || !p || !check_buffers(p, bp, bm, ntr, stride)) return nullptr;
     if (!p->cstream) {
         if (!ok(hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking), "hipStreamCreate(halo)") ||
             !ok(hipEventCreateWithFlags(&p->ev_ready, hipEventDisableTiming), "hipEventCreate(halo)") ||
@@ -216,7 +235,7 @@ hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm,
     if (!ok(hipEventRecord(p->ev_ready, s), "hipEventRecord(halo ready)") ||
         !ok(hipStreamWaitEvent(p->cstream, p->ev_ready, 0), "hipStreamWaitEvent(halo ready)"))
         return nullptr;
-    if (!exchange_on(c, p, bp, bm, p->cstream)) return nullptr;
+    if (!exchange_on(c, p, bp, bm, ntr, stride, p->cstream)) return nullptr;
     if (!ok(hipEventRecord(p->ev_done, p->cstream), "hipEventRecord(halo done)")) return nullptr;
     return p->ev_done;
 }
@@ -231,8 +250,21 @@ void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void 
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
     Buffer *bp = buf(fct_plus, "fct_plus"), *bm = buf(fct_minus, "fct_minus");
-    if (!c || !p || !bp || !bm || !check_buffers(p, bp, bm)) return;
-    if (exchange_on(c, p, bp, bm, stream_of(s))) *istat = 0;
+    if (!c || !p || !bp || !bm || !check_buffers(p, bp, bm, 1, 0)) return;
+    if (exchange_on(c, p, bp, bm, 1, 0, stream_of(s))) *istat = 0;
+}
+
+void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
+                                   int *nod_columns, void **fct_plus, void **fct_minus)
+{
+    *istat = 1;
+    Comm *c = comm_of(comm);
+    HaloPlan *p = plan_of(plan);
+    Buffer *bp = buf(fct_plus, "fct_plus"), *bm = buf(fct_minus, "fct_minus");
+    if (!c || !p || !bp || !bm) return;
+    const size_t stride = (size_t)(*nod_columns) * p->L;
+    if (!check_buffers(p, bp, bm, *ntracers, stride)) return;
+    if (exchange_on(c, p, bp, bm, *ntracers, stride, stream_of(s))) *istat = 0;
 }
 
 }  // extern "C"

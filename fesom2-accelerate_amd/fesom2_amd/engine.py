@@ -202,6 +202,86 @@ class FctAle:
         self.h = {}
 
 
+TRACER_FIELDS = ("ttf", "LO", "del_v", "del_h", "plus", "minus", "adf_v", "adf_h")
+SHARED_FIELDS = ("area", "area_inv", "hnode", "hnode_new")
+
+
+class FctAleBatch(FctAle):
+    """``ntracers`` tracers on one mesh through the batched entry points
+    (``fct_ale_pre_comm_batched_acc_`` / ``fct_ale_post_comm_c_batched_acc_``).
+
+    ``tracers`` is a list of field dicts (:func:`fesom2_amd.synth.make_tracer_fields`); the mesh
+    fields (area, area_inv, hnode, hnode_new) are taken from the first.  Per-tracer arrays are
+    stacked tracer-slowest, i.e. Fortran ``(nl-1, nod, ntracers)``.
+    """
+
+    def __init__(self, dmesh: DeviceMesh, tracers, stream=None, vlimit=1, flux_eps=1e-16, bignumber=1e3, dt=1.0):
+        m = dmesh.m
+        self.dm, self.m, self.ntr = dmesh, m, len(tracers)
+        self.stream = stream or abi.Stream()
+        self.vlimit, self.eps, self.big, self.dt = vlimit, flux_eps, bignumber, dt
+        NT, L = m.N + m.H, m.L
+        self.host = {}
+        for k in TRACER_FIELDS:
+            parts = [np.asarray(t[k], np.float64) if k in t else np.zeros(NT * L) for t in tracers]
+            self.host[k] = np.ascontiguousarray(np.concatenate(parts))
+        for k in SHARED_FIELDS:
+            self.host[k] = np.ascontiguousarray(tracers[0][k], dtype=np.float64).copy()
+        self.h = {}
+        events = {"ttf", "adf_v", "adf_h"}
+        for name, a in self.host.items():
+            h = abi.Handle(name)
+            st = C.c_int(0)
+            dll().alloc_var_(h.ref, arr(a), ip(a.size), bp(name in events), C.byref(st))
+            check(st, f"alloc_var_({name})")
+            self.h[name] = h
+            dll().transfer_var_(h.ref, arr(a))
+
+    def pre_comm(self):
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_pre_comm_batched_acc_(
+            C.byref(st), self.stream.ref, ip(self.ntr), h["plus"].ref, h["minus"].ref, h["ttf"].ref, h["LO"].ref,
+            h["adf_v"].ref, h["adf_h"].ref, h["area_inv"].ref, ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl),
+            d["nlev_nod"].ref, d["nlev_elem"].ref, d["elem2D_nodes"].ref, d["nie_num"].ref, d["nie"].ref, ip(m.dim),
+            d["edges"].ref, d["edge_tri"].ref, ip(self.vlimit), dp(self.eps), dp(self.big), dp(self.dt))
+        return st.value
+
+    def _phase2_args(self):
+        m, h, d = self.m, self.h, self.dm.h
+        return (h["plus"].ref, h["minus"].ref, h["adf_v"].ref, h["adf_h"].ref, h["del_v"].ref, h["del_h"].ref,
+                h["ttf"].ref, h["LO"].ref, h["hnode"].ref, h["hnode_new"].ref, h["area"].ref, ip(m.N), ip(m.H),
+                ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref, d["edges"].ref, d["edge_tri"].ref,
+                dp(self.dt))
+
+    def post_comm_c(self):
+        st = C.c_int(-1)
+        dll().fct_ale_post_comm_c_batched_acc_(C.byref(st), self.stream.ref, ip(self.ntr), *self._phase2_args())
+        return st.value
+
+    def exchange(self, comm, plan):
+        st = C.c_int(-1)
+        dll().fct_ale_exchange_batched_acc_(C.byref(st), self.stream.ref, comm.ref, plan.ref, ip(self.ntr),
+                                            ip(self.m.N + self.m.H), self.h["plus"].ref, self.h["minus"].ref)
+        check(st, "fct_ale_exchange_batched_acc_")
+
+    def exchange_post_comm_c(self, comm, plan):
+        st = C.c_int(-1)
+        dll().fct_ale_exchange_post_comm_c_batched_acc_(C.byref(st), self.stream.ref, comm.ref, plan.ref,
+                                                        ip(self.ntr), *self._phase2_args())
+        return st.value
+
+    def full_pass(self, fused=True):
+        s1 = self.pre_comm()
+        return self.post_comm_c() if s1 == 6 else s1
+
+    def tracer(self, name, k):
+        """Tracer k's slice of a downloaded per-tracer field."""
+        a = self.download(name)
+        n = a.size // self.ntr
+        return a[k * n:(k + 1) * n]
+
+
 class Halo:
     """RCCL communicator and halo plan of one rank (fesom2_comm_* / fesom2_halo_plan_).
 

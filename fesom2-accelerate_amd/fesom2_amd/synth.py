@@ -147,6 +147,16 @@ def make_fields(m: Mesh, seed=43, area_scale=1.0, adf_scale=0.5):
     return f
 
 
+def make_tracer_fields(m: Mesh, ntracers, seed=43, **kw):
+    """Fields of ``ntracers`` tracers (seeds 43+k); the mesh fields (area, area_inv,
+    hnode, hnode_new) of every tracer are those of the first, as one ocean state shares them."""
+    out = [make_fields(m, seed=seed + k, **kw) for k in range(ntracers)]
+    for f in out[1:]:
+        for name in ("area", "area_inv", "hnode", "hnode_new"):
+            f[name] = out[0][name]
+    return out
+
+
 def permute_mesh(m: Mesh, seed=7):
     """Shuffle node, element and edge numbering (an 'unstructured' stress variant).
 

@@ -182,6 +182,41 @@ void fct_ale_exchange_post_comm_c_acc_(int *alg_state, void **s, void **comm, vo
                                        void **nlevels_nod2D, void **nlevels_elem2D,
                                        void **nod2D_edges, void **elem2D_edges, real_type *dt);
 
+/* ---- multi-tracer batched variant (SURVEY.md 8(b) "new exports": several tracers per launch).
+ * Per-tracer handles hold ntracers tracers one after another: ttf, fct_LO, fct_plus, fct_minus,
+ * del_ttf_advvert, del_ttf_advhoriz (myDim_nod2D+eDim_nod2D)*(nl-1) doubles apart, fct_adf_v
+ * (myDim_nod2D+eDim_nod2D)*nl apart, fct_adf_h myDim_edge2D*(nl-1) apart -- i.e. Fortran arrays
+ * (nl-1, nod, ntracers), (nl, nod, ntracers), (nl-1, edge, ntracers).  Mesh fields (area,
+ * area_inv, hnode, hnode_new) are shared.  Each tracer's results equal a single-tracer pass on
+ * its slice.  Fused path only. */
+void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                   void **fct_minus, void **ttf, void **fct_LO, void **fct_adf_v,
+                                   void **fct_adf_h, void **area_inv, int *myDim_nod2D,
+                                   int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                                   void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                                   void **nod_in_elem2D_num, void **nod_in_elem2D,
+                                   int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges,
+                                   int *vlimit, real_type *flux_eps, real_type *bignumber,
+                                   real_type *dt);
+void fct_ale_post_comm_c_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                      void **fct_minus, void **fct_adf_v, void **fct_adf_h,
+                                      void **del_ttf_advvert, void **del_ttf_advhoriz, void **ttf,
+                                      void **fct_LO, void **hnode, void **hnode_new, void **area,
+                                      int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                      void **nlevels_nod2D, void **nlevels_elem2D,
+                                      void **nod2D_edges, void **elem2D_edges, real_type *dt);
+/* nod_columns = myDim_nod2D + eDim_nod2D (the per-tracer stride in columns). */
+void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
+                                   int *nod_columns, void **fct_plus, void **fct_minus);
+void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
+                                               int *ntracers, void **fct_plus, void **fct_minus,
+                                               void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,
+                                               void **del_ttf_advhoriz, void **ttf, void **fct_LO,
+                                               void **hnode, void **hnode_new, void **area,
+                                               int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D,
+                                               int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
+                                               void **nod2D_edges, void **elem2D_edges, real_type *dt);
+
 #ifdef __cplusplus
 }
 #endif

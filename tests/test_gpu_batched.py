@@ -1,0 +1,172 @@
+"""GPU: the multi-tracer batched entry points (fct_ale_pre_comm_batched_acc_,
+fct_ale_post_comm_c_batched_acc_, the batched exchanges) against the oracle, one single-tracer
+oracle pass per tracer slice (SURVEY.md 8(b) "multi-tracer batched variant", BASELINE config 3).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import assert_cols_equal
+from fesom2_amd import abi, engine, partition, synth
+from fesom2_amd.abi import arr, dll, ip
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    abi.set_mpi_rank(0, 1)
+    abi.set_resident(True)
+    abi.set_path("fused")
+    yield
+
+
+def check_tracer(m, e, k, want):
+    L = m.L
+    NT = m.N + m.H
+    assert_cols_equal(e.tracer("plus", k)[: m.N * L], want["plus"][: m.N * L], m.nlev_nod, L, m.N, f"plus[{k}]")
+    assert_cols_equal(e.tracer("minus", k)[: m.N * L], want["minus"][: m.N * L], m.nlev_nod, L, m.N, f"minus[{k}]")
+    for name, n in (("adf_v", m.N * m.nl), ("del_v", m.N * L), ("del_h", m.N * L), ("adf_h", m.E * L)):
+        got, w = e.tracer(name, k)[:n], want[name][:n]
+        bad = np.flatnonzero(got != w)
+        assert bad.size == 0, f"{name}[{k}]: {bad.size} differ, first at {bad[:5]}"
+    assert NT * L * e.ntr == e.host["plus"].size
+
+
+@pytest.mark.parametrize("name,ntr", [("tiny", 2), ("8k x 20", 1), ("8k x 20", 3), ("8k x 20", 6),
+                                      ("127k x 47", 6)])
+@pytest.mark.parametrize("resident", [True, False])
+def test_batched_pass_matches_per_tracer_oracle(name, ntr, resident):
+    m = synth.config_mesh(name)
+    tracers = synth.make_tracer_fields(m, ntr)
+    abi.set_resident(resident)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.full_pass() == 9, abi.last_error()
+        e.sync()
+        for k in range(ntr):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+    finally:
+        abi.set_resident(True)
+        e.free()
+        dm.free()
+
+
+def test_batched_tracers_differ_and_match_single_entry():
+    """Tracer k of a batch equals the single-tracer entry points on tracer k's fields."""
+    m = synth.config_mesh("8k x 20")
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    eb = engine.FctAleBatch(dm, tracers)
+    singles = [engine.FctAle(dm, t) for t in tracers]
+    try:
+        assert eb.full_pass() == 9
+        for s in singles:
+            assert s.full_pass() == 9
+        eb.sync()
+        for k, s in enumerate(singles):
+            s.sync()
+            for name in ("del_v", "del_h", "adf_v", "adf_h"):
+                assert np.array_equal(eb.tracer(name, k), s.download(name)), (name, k)
+        assert not np.array_equal(eb.tracer("del_h", 0), eb.tracer("del_h", 1))
+    finally:
+        eb.free()
+        for s in singles:
+            s.free()
+        dm.free()
+
+
+def test_batched_rejects_short_buffers():
+    m = synth.config_mesh("tiny")
+    tracers = synth.make_tracer_fields(m, 2)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        e.ntr = 3  # buffers hold 2 tracers
+        assert e.pre_comm() == 0
+        assert "holds" in abi.last_error() or "bytes" in abi.last_error()
+        assert e.post_comm_c() != 9
+    finally:
+        e.free()
+        dm.free()
+
+
+@pytest.fixture(scope="module")
+def comm():
+    uid = engine.Halo.unique_id()
+    h = abi.Handle("comm")
+    st = C.c_int(0)
+    dll().fesom2_comm_init_(h.ref, uid, ip(0), ip(1), C.byref(st))
+    abi.check(st, "fesom2_comm_init_")
+    yield h
+    dll().fesom2_comm_free_(h.ref)
+
+
+def make_plan(send, recv, nl):
+    h = abi.Handle("plan")
+    st = C.c_int(0)
+    dll().fesom2_halo_plan_(h.ref, ip(1), arr(np.zeros(1, np.int32)), arr(np.array([send.size], np.int32)),
+                            arr(np.ascontiguousarray(send, np.int32)), arr(np.array([recv.size], np.int32)),
+                            arr(np.ascontiguousarray(recv, np.int32)), ip(nl), C.byref(st))
+    abi.check(st, "fesom2_halo_plan_")
+    return h
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_batched_partitioned_exchange(comm, overlap):
+    """Two partitions, 3 tracers: after phase 1 each partition's halo columns get the neighbour's
+    values, stored deranged (c_j holds the value of c_{j+1}) for every tracer; a one-rank plan
+    sending c_j into c_{j+1} restores them -- through fct_ale_exchange_batched_acc_ then the batched
+    phase 2, or the overlapped batched entry.  Owned results equal the global oracle per tracer."""
+    nx, ny, nl, ntr = 64, 48, 21, 3
+    g = synth.make_mesh(nx, ny, nl)
+    gtr = synth.make_tracer_fields(g, ntr)
+    wants = [O.full_pass(g, t) for t in gtr]
+    part = partition.strip_parts(nx, ny, 2)
+    locs = [partition.local_mesh(g, part, r) for r in range(2)]
+    runs, plans, outs, pm = [], [], [], []
+    L = g.L
+    try:
+        for m, _ in locs:
+            dm = engine.DeviceMesh(m)
+            runs.append((dm, engine.FctAleBatch(dm, synth.make_tracer_fields(m, ntr))))
+        for _, e in runs:
+            assert e.pre_comm() == 6
+            e.sync()
+            pm.append([e.download("plus").reshape(ntr, -1, L), e.download("minus").reshape(ntr, -1, L)])
+        for r, (m, h) in enumerate(locs):
+            for q in h.neighbors:
+                src, dst = locs[q][1].send[r] - 1, h.recv[q] - 1
+                for a in range(2):
+                    pm[r][a][:, dst] = pm[q][a][:, src]
+            cols = np.arange(m.N, m.N + m.H)
+            nxt = np.roll(cols, -1)
+            for a, name in enumerate(("plus", "minus")):
+                stored = pm[r][a].copy()
+                stored[:, cols] = pm[r][a][:, nxt]
+                runs[r][1].upload(name, stored.reshape(-1))
+            plans.append(make_plan(cols + 1, nxt + 1, nl))
+        for (_, e), plan in zip(runs, plans):
+            if overlap:
+                assert e.exchange_post_comm_c(comm, plan) == 9, abi.last_error()
+            else:
+                e.exchange(comm, plan)
+                assert e.post_comm_c() == 9, abi.last_error()
+        for _, e in runs:
+            e.sync()
+            outs.append({k: e.download(k) for k in ("del_v", "del_h", "adf_v")})
+    finally:
+        for plan in plans:
+            dll().fesom2_halo_plan_free_(plan.ref)
+        for dm, e in runs:
+            e.free()
+            dm.free()
+    ms = [m for m, _ in locs]
+    for k in range(ntr):
+        for name, w in (("del_v", L), ("del_h", L), ("adf_v", nl)):
+            got = partition.gather_owned(ms, lambda r: outs[r][name].reshape(ntr, -1)[k], w, g.N)
+            assert np.array_equal(got, wants[k][name]), (name, k)

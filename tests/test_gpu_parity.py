@@ -83,6 +83,23 @@ def test_full_pass_matches_oracle(name, full, perm, fused, path):
     check_pass(m, got, want)
 
 
+KNOBS = [{"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "0"}, {"FESOM2_B3H_U": "4", "FESOM2_B3H_NT": "0"},
+         {"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "1"}, {"FESOM2_B3H_CPT": "4"}, {"FESOM2_NT": "3"},
+         {"FESOM2_P1_BATCH": "44", "FESOM2_P2_BATCH": "8"}, {"FESOM2_PATCH": "0"}, {"FESOM2_PATCH": "7"}]
+
+
+@pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_kernel_variants_match_oracle(knobs, name, monkeypatch):
+    """Every tuning variant the launchers can select (env knobs read at launch) is exact too."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    m, f = mesh(name)
+    st, got = run_pass(m, f)
+    assert st == 9
+    check_pass(m, got, O.full_pass(m, f))
+
+
 @pytest.mark.parametrize("vlimit", [2, 3])
 @pytest.mark.parametrize("path", ["fused", "stepwise"])
 def test_vlimit_variants(vlimit, path):
