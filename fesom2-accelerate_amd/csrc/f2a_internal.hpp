@@ -125,6 +125,23 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
+// iter_yn phase 2 (docs/refactoring.md:227-229, :258-260, :265-290): node kernel = b3v writing
+// fct_adf_v2, LO update from the limited vertical and horizontal fluxes (recomputed in-thread from
+// plus/minus of both edge endpoints), then fct_adf_v <- fct_adf_v2 over the whole column; the
+// edge kernel (after it) writes fct_adf_h2 = (1-ae) adf_h and fct_adf_h <- fct_adf_h2.
+struct P2IterArgs {
+    int nl;
+    const NodeRec *nodes;
+    int count;
+    const int *edges;  // nod2D_edges (2, E), 1-based: the other endpoint of an edge
+    const real *plus, *minus, *hnode_new, *area, *adf_h;
+    real *LO, *adf_v, *adf_v2;
+    real dt;
+    Tracers tr;
+};
+hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s);
+hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
+                           real *adf_h2, const Tracers &tr, hipStream_t s);
 // columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
 int group_columns(int L);
 

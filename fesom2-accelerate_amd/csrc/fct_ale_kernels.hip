@@ -915,6 +915,153 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
+// iter_yn phase 2, nodes (see P2IterArgs).  Every slot of a column also copies fct_adf_v2 into
+// fct_adf_v for the levels the iteration does not assign (nz = 1, the bottom interface and the dry
+// levels: the Fortran's whole-array `fct_adf_v = fct_adf_v2`); the last slot covers level nl-1.
+template <int C>
+__global__ __launch_bounds__(1024) void k_p2_iter(MeshPlanDev mp, P2IterArgs a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G]
+    const int L = a.nl - 1, S = L / C;
+    const int t = threadIdx.x;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_v2 += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int Ln = ni.Ln;
+    const int top = Ln > 1 ? Ln : 1;
+    const int na = col ? max(0, min(C, top - z0)) : 0;
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;
+    real rem[C], lo[C];
+    const size_t b = (size_t)ni.n * L + z0, ab = (size_t)ni.n * a.nl + z0;
+#pragma unroll
+    for (int c = 0; c < C; c++) rem[c] = lo[c] = 0.;
+    if (na > 0) {
+        real pp[C + 2], mm[C + 2], f[C + 1];
+        pp[0] = z0 ? a.plus[b - 1] : 0.;
+        mm[0] = z0 ? a.minus[b - 1] : 0.;
+        {
+            real tp[C], tmn[C];
+            ldv<C>(a.plus + b, tp);
+            ldv<C>(a.minus + b, tmn);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                pp[c + 1] = tp[c];
+                mm[c + 1] = tmn[c];
+            }
+        }
+        const bool below = z0 + C < Ln;
+        pp[C + 1] = below ? a.plus[b + C] : 0.;
+        mm[C + 1] = below ? a.minus[b + C] : 0.;
+#pragma unroll
+        for (int c = 0; c <= C; c++) f[c] = a.adf_v[ab + c];
+        real lim[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) {
+            const int z = z0 + c;
+            const bool lim_here = (c < C) ? (z < top) : (z < Ln);
+            const real ae = lim_here ? b3v_factor(z, f[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) : 1.0;
+            lim[c] = lim_here ? ae * f[c] : f[c];
+            if (c < C) rem[c] = (1.0 - ae) * f[c];  // written for 1 <= z < Ln only
+        }
+        if (nw > 0) {
+            real hnn[C], ar[C];
+            ldv<C>(a.LO + b, lo);
+            ldv<C>(a.hnode_new + b, hnn);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                ar[c] = c < nw ? a.area[ab + c] : 1.0;
+                // LO + (adf_v(nz) - adf_v(nz+1)) * dt / area / hnode_new, left to right
+                if (c < nw) lo[c] = lo[c] + (lim[c] - lim[c + 1]) * a.dt / ar[c] / hnn[c];
+            }
+            const int ne = ni.e1 - ni.e0;
+            for (int k = 0; k < ne; k++) {  // ascending edge order, as the Fortran edge loop
+                const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+                const int lev = er.code >> 1, second = er.code & 1;
+                if (z0 >= lev) continue;
+                const int other = a.edges[2 * er.edge + (second ? 0 : 1)] - 1;
+                real h[C], po[C], mo[C];
+                ldv<C>(a.adf_h + (size_t)er.edge * L + z0, h);
+                ldv<C>(a.plus + (size_t)other * L + z0, po);
+                ldv<C>(a.minus + (size_t)other * L + z0, mo);
+#pragma unroll
+                for (int c = 0; c < C; c++) {
+                    if (z0 + c >= lev) continue;
+                    const real ae = second ? b3h_factor(h[c], po[c], mo[c], pp[c + 1], mm[c + 1])
+                                           : b3h_factor(h[c], pp[c + 1], mm[c + 1], po[c], mo[c]);
+                    const real lh = ae * h[c];
+                    lo[c] = second ? lo[c] - lh * a.dt / ar[c] / hnn[c] : lo[c] + lh * a.dt / ar[c] / hnn[c];
+                }
+            }
+        }
+    }
+    __syncthreads();  // every raw fct_adf_v read of the block precedes the writes
+    if (!col) return;
+    if (nw > 0) stv<C>(a.LO + b, lo, nw);
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        const int z = z0 + c;
+        if (z >= 1 && z < Ln) {
+            a.adf_v2[ab + c] = rem[c];
+            a.adf_v[ab + c] = rem[c];
+        } else {
+            a.adf_v[ab + c] = a.adf_v2[ab + c];
+        }
+    }
+    if (z0 + C == L) a.adf_v[ab + C] = a.adf_v2[ab + C];  // level nl-1 (never wet)
+}
+
+// iter_yn phase 2, edges (after k_p2_iter has read the raw fluxes): fct_adf_h2 = (1-ae) adf_h on
+// the edge's levels, then fct_adf_h <- fct_adf_h2 on every level.
+template <int C>
+__global__ __launch_bounds__(1024) void k_b3h_iter(const int4 *__restrict__ einfo, int n_edges, int L,
+                                                   int G, float invS, const real *__restrict__ plus,
+                                                   const real *__restrict__ minus,
+                                                   real *__restrict__ adf_h, real *__restrict__ adf_h2,
+                                                   Tracers trs)
+{
+    int j, u, tr;
+    slot_of(threadIdx.x, L / C, invS, j, u);
+    const int z0 = C * u;
+    const int k = group_tracer(trs.n, tr, c_tracer_major & 2) * G + j;
+    if (j >= G || k >= n_edges) return;
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
+    adf_h2 += tr * trs.edge;
+    const int4 ei = einfo[k];
+    const size_t i = (size_t)ei.w * L + z0;
+    const size_t i1 = (size_t)ei.x * L + z0, i2 = (size_t)ei.y * L + z0;
+    real f[C], h2[C], p1[C], m1[C], p2[C], m2[C];
+    ldv<C>(adf_h + i, f);
+    ldv<C>(adf_h2 + i, h2);
+    if (z0 < ei.z) {
+        ldv<C>(plus + i1, p1);
+        ldv<C>(minus + i1, m1);
+        ldv<C>(plus + i2, p2);
+        ldv<C>(minus + i2, m2);
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++)
+        if (z0 + c < ei.z) h2[c] = (1.0 - b3h_factor(f[c], p1[c], m1[c], p2[c], m2[c])) * f[c];
+    stv<C>(adf_h2 + i, h2, C);
+    stv<C>(adf_h + i, h2, C);
+}
+
 // columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads)
 int group_columns(int S)
 {
@@ -1153,6 +1300,29 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
         F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
     }
     F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+}
+
+hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec);
+    if (C == 2) F2A_LAUNCH_GROUPS((k_p2_iter<2>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2_iter<1>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
+                           real *adf_h2, const Tracers &tr, hipStream_t s)
+{
+    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(mp.n_edges + G - 1) / G * tr.n;
+    const float invS = 1.0f / (float)S;
+    if (C == 2)
+        F2A_LAUNCH_GROUPS((k_b3h_iter<2>), groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus,
+                          adf_h, adf_h2, tr);
+    F2A_LAUNCH_GROUPS((k_b3h_iter<1>), groups, G, S, 0, s, mp.p_edge_info, mp.n_edges, L, G, invS, plus, minus, adf_h,
+                      adf_h2, tr);
 }
 
 hipError_t launch_halo_pack(const int *nodes, int count, int L, int ntr, size_t stride, const real *plus,

@@ -470,6 +470,105 @@ void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **
                      "fct_ale_exchange_post_comm_c_batched_acc_");
 }
 
+// iter_yn phase 2 (docs/refactoring.md:227-229, :258-260, :265-290): b3 limiting with the
+// remainders (1-ae)*flux into fct_adf_v2/fct_adf_h2, fct_LO updated with the limited fluxes, then
+// fct_adf_v <- fct_adf_v2 and fct_adf_h <- fct_adf_h2 (whole arrays, as the Fortran assignment);
+// the caller runs the next fct_ale iteration.  alg_state -> 9.
+static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_plus, void **fct_minus,
+                                void **fct_adf_v, void **fct_adf_h, void **fct_adf_v2, void **fct_adf_h2,
+                                void **fct_LO, void **hnode_new, void **area, int *myDim_nod2D,
+                                int *eDim_nod2D, int *myDim_edge2D, int *nl, void **nlevels_nod2D,
+                                void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges, real *dt,
+                                const char *who)
+{
+    *alg_state = 0;
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
+    if (!check_levels(NL, who)) return;
+    if (ntr < 1) {
+        report("%s: ntracers = %d", who, ntr);
+        return;
+    }
+    const bool batched = ntr > 1;
+    const size_t node_b = batched ? col_bytes(NT, L) * ntr : col_bytes(N, L);
+    const size_t lev_b = batched ? col_bytes(NT, NL) * ntr : col_bytes(N, NL);
+    Buffer *bplus = need(fct_plus, col_bytes(NT, L) * ntr, "fct_plus");
+    Buffer *bminus = need(fct_minus, col_bytes(NT, L) * ntr, "fct_minus");
+    Buffer *badfv = need(fct_adf_v, lev_b, "fct_adf_v"), *badfv2 = need(fct_adf_v2, lev_b, "fct_adf_v2");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L) * ntr, "fct_adf_h");
+    Buffer *badfh2 = need(fct_adf_h2, col_bytes(E, L) * ntr, "fct_adf_h2");
+    Buffer *blo = need(fct_LO, node_b, "fct_LO");
+    Buffer *bhn = need(hnode_new, col_bytes(N, L), "hnode_new"), *barea = need(area, col_bytes(N, NL), "area");
+    Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    if (!bplus || !bminus || !badfv || !badfv2 || !badfh || !badfh2 || !blo || !bhn || !barea || !bnl || !mh.edges ||
+        !mh.edge_tri || !mh.nlev_elem)
+        return;
+    mh.nlev_nod = bnl;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    if (!plan) return;
+    const f2a::MeshPlanDev &d = plan->dev;
+    if (!g_resident) {
+        for (Buffer *b : {bplus, bminus, blo, badfv2, badfh2})
+            if (!h2d(b, false, st, false)) return;
+    }
+    const f2a::Tracers trs{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    f2a::P2IterArgs a{NL, d.p2_rec, N, dptr<int>(mh.edges), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(bhn),
+                      dptr<real>(barea), dptr<real>(badfh), dptr<real>(blo), dptr<real>(badfv), dptr<real>(badfv2),
+                      *dt, trs};
+    if (!run("fct_ale_p2_iter", st, [&] { return f2a::launch_p2_iter(d, a, st); })) return;
+    if (!run("fct_ale_b3_horizontal_iter", st, [&] {
+            return f2a::launch_b3h_iter(d, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
+                                        dptr<real>(badfh2), trs, st);
+        }))
+        return;
+    // halo columns of the whole-array fct_adf_v <- fct_adf_v2 (where the handles hold them)
+    const size_t need_halo = col_bytes(NT, NL) * ntr;
+    if (NT > N && badfv->size >= need_halo && badfv2->size >= need_halo)
+        for (int k = 0; k < ntr; k++) {
+            const size_t off = (size_t)k * NT * NL + (size_t)N * NL;
+            if (!ok(hipMemcpyAsync(dptr<real>(badfv) + off, dptr<real>(badfv2) + off, col_bytes(NT - N, NL),
+                                   hipMemcpyDeviceToDevice, st),
+                    "hipMemcpyAsync(fct_adf_v halo)"))
+                return;
+        }
+    *alg_state = 9;
+    if (!g_resident)
+        for (Buffer *b : {blo, badfv, badfv2, badfh, badfh2})
+            if (!d2h_async(b, st)) {
+                *alg_state = 0;
+                return;
+            }
+}
+
+void fct_ale_post_comm_iter_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                                 void **fct_adf_v, void **fct_adf_h, void **fct_adf_v2,
+                                 void **fct_adf_h2, void **fct_LO, void **hnode_new, void **area,
+                                 int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                 void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges,
+                                 void **elem2D_edges, real *dt)
+{
+    post_comm_iter_impl(alg_state, s, 1, fct_plus, fct_minus, fct_adf_v, fct_adf_h, fct_adf_v2, fct_adf_h2, fct_LO,
+                        hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D, nlevels_elem2D,
+                        nod2D_edges, elem2D_edges, dt, "fct_ale_post_comm_iter_acc_");
+}
+
+void fct_ale_post_comm_iter_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                         void **fct_minus, void **fct_adf_v, void **fct_adf_h,
+                                         void **fct_adf_v2, void **fct_adf_h2, void **fct_LO,
+                                         void **hnode_new, void **area, int *myDim_nod2D,
+                                         int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                         void **nlevels_nod2D, void **nlevels_elem2D,
+                                         void **nod2D_edges, void **elem2D_edges, real *dt)
+{
+    post_comm_iter_impl(alg_state, s, *ntracers, fct_plus, fct_minus, fct_adf_v, fct_adf_h, fct_adf_v2, fct_adf_h2,
+                        fct_LO, hnode_new, area, myDim_nod2D, eDim_nod2D, myDim_edge2D, nl, nlevels_nod2D,
+                        nlevels_elem2D, nod2D_edges, elem2D_edges, dt, "fct_ale_post_comm_iter_batched_acc_");
+}
+
 // ----------------------------------------------------------------------------- utilities
 
 void fesom2_set_resident_(int *resident) { g_resident = (resident && *resident) ? 1 : 0; }

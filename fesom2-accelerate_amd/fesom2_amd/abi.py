@@ -28,7 +28,8 @@ EXPORTS = (
     "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_halo_plan_",
     "fesom2_halo_plan_free_", "fct_ale_exchange_acc_", "fct_ale_exchange_post_comm_c_acc_",
     "fct_ale_pre_comm_batched_acc_", "fct_ale_post_comm_c_batched_acc_", "fct_ale_exchange_batched_acc_",
-    "fct_ale_exchange_post_comm_c_batched_acc_",
+    "fct_ale_exchange_post_comm_c_batched_acc_", "fct_ale_post_comm_iter_acc_",
+    "fct_ale_post_comm_iter_batched_acc_",
 )
 
 _dll = None

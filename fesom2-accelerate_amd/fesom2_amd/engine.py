@@ -144,6 +144,42 @@ class FctAle:
             d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
         return st.value
 
+    def _iter_buffers(self):
+        """fct_adf_v2 / fct_adf_h2 (zero-initialised, as FESOM allocates them) on first use."""
+        for name, like in (("adf_v2", "adf_v"), ("adf_h2", "adf_h")):
+            if name not in self.h:
+                a = np.zeros_like(self.host[like])
+                self.host[name] = a
+                h = abi.Handle(name)
+                st = C.c_int(0)
+                dll().alloc_var_(h.ref, arr(a), ip(a.size), bp(False), C.byref(st))
+                check(st, f"alloc_var_({name})")
+                dll().transfer_var_(h.ref, arr(a))
+                self.h[name] = h
+
+    def post_comm_iter(self):
+        """iter_yn phase 2 (fct_ale_post_comm_iter_acc_): LO updated, adf <- remainders."""
+        self._iter_buffers()
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_post_comm_iter_acc_(
+            C.byref(st), self.stream.ref, h["plus"].ref, h["minus"].ref, h["adf_v"].ref, h["adf_h"].ref,
+            h["adf_v2"].ref, h["adf_h2"].ref, h["LO"].ref, h["hnode_new"].ref, h["area"].ref, ip(m.N), ip(m.H),
+            ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref, d["edges"].ref, d["edge_tri"].ref,
+            dp(self.dt))
+        return st.value
+
+    def iterated_pass(self, iterations):
+        """``iterations - 1`` iter_yn rounds then the final fused pass (final alg_state)."""
+        for _ in range(iterations - 1):
+            s1 = self.pre_comm()
+            if s1 != 6:
+                return s1
+            s2 = self.post_comm_iter()
+            if s2 != 9:
+                return s2
+        return self.full_pass()
+
     def exchange(self, comm, plan):
         """fct_ale_exchange_acc_: RCCL halo exchange of fct_plus/fct_minus on this stream."""
         st = C.c_int(-1)
@@ -274,6 +310,17 @@ class FctAleBatch(FctAle):
     def full_pass(self, fused=True):
         s1 = self.pre_comm()
         return self.post_comm_c() if s1 == 6 else s1
+
+    def post_comm_iter(self):
+        self._iter_buffers()
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_post_comm_iter_batched_acc_(
+            C.byref(st), self.stream.ref, ip(self.ntr), h["plus"].ref, h["minus"].ref, h["adf_v"].ref,
+            h["adf_h"].ref, h["adf_v2"].ref, h["adf_h2"].ref, h["LO"].ref, h["hnode_new"].ref, h["area"].ref,
+            ip(m.N), ip(m.H), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref, d["edges"].ref,
+            d["edge_tri"].ref, dp(self.dt))
+        return st.value
 
     def tracer(self, name, k):
         """Tracer k's slice of a downloaded per-tracer field."""

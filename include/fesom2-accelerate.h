@@ -217,6 +217,26 @@ void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **
                                                int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                                                void **nod2D_edges, void **elem2D_edges, real_type *dt);
 
+/* ---- iter_yn iterative FCT (docs/refactoring.md:227-229, :258-260, :265-290).
+ * Phase 2 of a non-final iteration, after the exchange of fct_plus/minus: b3 limiting with the
+ * remainders fct_adf_v2 = (1-ae) fct_adf_v (levels 2..nlevels-1) and fct_adf_h2 = (1-ae) fct_adf_h,
+ * fct_LO += the limited flux divergence / hnode_new (owned nodes; halo entries of fct_LO are left
+ * alone -- the caller's LO halo exchange refreshes them), then fct_adf_v <- fct_adf_v2 and
+ * fct_adf_h <- fct_adf_h2.  No c-step; the caller runs fct_ale again.  alg_state -> 9. */
+void fct_ale_post_comm_iter_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
+                                 void **fct_adf_v, void **fct_adf_h, void **fct_adf_v2,
+                                 void **fct_adf_h2, void **fct_LO, void **hnode_new, void **area,
+                                 int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                 void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges,
+                                 void **elem2D_edges, real_type *dt);
+void fct_ale_post_comm_iter_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                         void **fct_minus, void **fct_adf_v, void **fct_adf_h,
+                                         void **fct_adf_v2, void **fct_adf_h2, void **fct_LO,
+                                         void **hnode_new, void **area, int *myDim_nod2D,
+                                         int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                                         void **nlevels_nod2D, void **nlevels_elem2D,
+                                         void **nod2D_edges, void **elem2D_edges, real_type *dt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -150,6 +150,39 @@ def post_comm(m, f, plus, minus, dt=1.0):
     return dict(adf_v=adf_v, adf_h=adf_h, del_v=del_v, del_h=del_h)
 
 
+def post_comm_iter(m, f, plus, minus, adf_v2, adf_h2, dt=1.0):
+    """iter_yn phase 2 of one non-final iteration (docs/refactoring.md:204-290 with iter_yn true):
+    b3v/b3h writing the remainders into copies of adf_v2/adf_h2, the LO update, then the Fortran's
+    whole-array assignments fct_adf_h = fct_adf_h2, fct_adf_v = fct_adf_v2.  Returns LO, adf_v,
+    adf_h, adf_v2, adf_h2 (parity unpinned: no executable reference holds this branch)."""
+    adf_v, adf_h = f["adf_v"].copy(), f["adf_h"].copy()
+    adf_v2, adf_h2 = adf_v2.copy(), adf_h2.copy()
+    LO = f["LO"].copy()
+    b3v(m.N, m.nlev_nod, m.nl, adf_v, plus, minus, adf_v2)
+    b3h(m.E, m.nlev_elem, m.nl, m.edges, m.edge_tri, adf_h, plus, minus, adf_h2)
+    lo_update(m.N, m.nlev_nod, m.E, m.nlev_elem, m.nl, m.edges, m.edge_tri, LO, adf_v, adf_h, dt, f["area"],
+              f["hnode_new"])
+    return dict(LO=LO, adf_v=adf_v2.copy(), adf_h=adf_h2.copy(), adf_v2=adf_v2, adf_h2=adf_h2)
+
+
+def iterated_pass(m, f, iterations, dt=1.0, **kw):
+    """FESOM2's iterative FCT on one domain: ``iterations - 1`` calls of fct_ale with iter_yn
+    (each updating LO and handing the remainders on as the next antidiffusive fluxes), then the
+    final non-iterative pass.  adf_v2/adf_h2 start at zero (FESOM allocates them zeroed)."""
+    f = dict(f)
+    adf_v2, adf_h2 = np.zeros_like(f["adf_v"]), np.zeros_like(f["adf_h"])
+    for _ in range(iterations - 1):
+        st, p1 = pre_comm(m, f, dt=dt, **kw)
+        if st != 5:
+            raise RuntimeError(f"oracle pre_comm stopped at alg_state {st}")
+        r = post_comm_iter(m, f, p1["plus"], p1["minus"], adf_v2, adf_h2, dt=dt)
+        f.update(LO=r["LO"], adf_v=r["adf_v"], adf_h=r["adf_h"])
+        adf_v2, adf_h2 = r["adf_v2"], r["adf_h2"]
+    out = full_pass(m, f, dt=dt, **kw)
+    out.update(LO=f["LO"], adf_v2=adf_v2, adf_h2=adf_h2)
+    return out
+
+
 def full_pass(m, f, vlimit=1, eps=1e-16, big=1e3, dt=1.0):
     """Single-domain full pass a1..c; returns dict with plus, minus, adf_v, adf_h, del_v, del_h."""
     st, p1 = pre_comm(m, f, vlimit=vlimit, eps=eps, big=big, dt=dt)

@@ -297,3 +297,73 @@ def test_reference_named_entries_run_on_gpu():
     want = O.pre_comm(m, f)[1]
     for k, v in (("ttf_max", tmax), ("ttf_min", tmin), ("plus", plus), ("minus", minus), ("UV", UV)):
         assert np.array_equal(v, want[k]), k
+
+
+@pytest.mark.parametrize("name", ["tiny", "8k x 20", "127k x 47"])
+@pytest.mark.parametrize("iterations", [2, 3])
+@pytest.mark.parametrize("resident", [True, False])
+def test_iter_yn_iterations_match_oracle(name, iterations, resident):
+    """iter_yn (docs/refactoring.md:227-290): iterations-1 rounds of fct_ale_post_comm_iter_acc_
+    (LO update + remainder hand-over) then the final pass; every array equals the oracle's
+    restatement of the Fortran (parity unpinned: no executable reference holds this branch)."""
+    m, f = mesh(name)
+    want = O.iterated_pass(m, f, iterations)
+    abi.set_resident(resident)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.iterated_pass(iterations) == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h", "LO", "adf_v2",
+                                          "adf_h2")}
+    finally:
+        abi.set_resident(True)
+        e.free()
+        dm.free()
+    check_pass(m, got, want)
+    for k in ("LO", "adf_v2", "adf_h2"):
+        bad = np.flatnonzero(got[k] != want[k])
+        assert bad.size == 0, f"{k}: {bad.size} differ, first at {bad[:5]}"
+
+
+def test_iter_yn_batched():
+    m = synth.config_mesh("8k x 20")
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.iterated_pass(2) == 9, abi.last_error()
+        e.sync()
+        for k in range(3):
+            want = O.iterated_pass(m, tracers[k], 2)
+            for name in ("LO", "adf_v", "adf_h", "del_v", "del_h", "adf_v2", "adf_h2"):
+                assert np.array_equal(e.tracer(name, k), want[name]), (name, k)
+    finally:
+        e.free()
+        dm.free()
+
+
+def test_iter_yn_whole_array_swap_keeps_unassigned_levels():
+    """Nonzero fct_adf_v2/fct_adf_h2 before the call: levels the iteration does not assign (nz=1,
+    bottom interface, dry levels) reach fct_adf_v/fct_adf_h through the whole-array assignment."""
+    m, f = mesh("8k x 20")
+    st, p1 = O.pre_comm(m, f)
+    rng = np.random.default_rng(5)
+    v2, h2 = rng.standard_normal(f["adf_v"].size), rng.standard_normal(f["adf_h"].size)
+    want = O.post_comm_iter(m, f, p1["plus"], p1["minus"], v2, h2)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        e._iter_buffers()
+        e.upload("adf_v2", v2)
+        e.upload("adf_h2", h2)
+        assert e.pre_comm() == 6
+        assert e.post_comm_iter() == 9, abi.last_error()
+        e.sync()
+        for k in ("LO", "adf_v", "adf_h", "adf_v2", "adf_h2"):
+            got = e.download(k)
+            bad = np.flatnonzero(got != want[k])
+            assert bad.size == 0, f"{k}: {bad.size} differ, first at {bad[:5]}"
+    finally:
+        e.free()
+        dm.free()

@@ -150,3 +150,73 @@ def test_empty_edge_set_and_minimum_levels():
     assert st == 5
     full = O.full_pass(m, f)
     assert np.isfinite(full["plus"]).all()
+
+
+def _fortran_iter_phase2(m, f, plus, minus, adf_v2, adf_h2, dt=1.0):
+    """docs/refactoring.md:204-290 with iter_yn true, transcribed statement by statement in plain
+    Python floats (1-based Fortran loops shifted to 0-based)."""
+    L, nl = m.L, m.nl
+    av, ah = list(f["adf_v"]), list(f["adf_h"])
+    av2, ah2, LO = list(adf_v2), list(adf_h2), list(f["LO"])
+    P, M, area, hnn = list(plus), list(minus), list(f["area"]), list(f["hnode_new"])
+    for n in range(m.N):
+        a, b = n * nl, n * L
+        ae = 1.0
+        ae = min(ae, P[b]) if av[a] >= 0.0 else min(ae, M[b])
+        av[a] = ae * av[a]
+        for z in range(1, int(m.nlev_nod[n]) - 1):
+            ae = 1.0
+            if av[a + z] >= 0.0:
+                ae = min(ae, M[b + z - 1]); ae = min(ae, P[b + z])
+            else:
+                ae = min(ae, P[b + z - 1]); ae = min(ae, M[b + z])
+            av2[a + z] = (1.0 - ae) * av[a + z]
+            av[a + z] = ae * av[a + z]
+    ed, et = m.edges.reshape(-1, 2) - 1, m.edge_tri.reshape(-1, 2)
+    lev = [max(int(m.nlev_elem[et[e, 0] - 1]) - 1, int(m.nlev_elem[et[e, 1] - 1]) - 1 if et[e, 1] > 0 else 0)
+           for e in range(m.E)]
+    for e in range(m.E):
+        n1, n2 = ed[e]
+        for z in range(lev[e]):
+            i = e * L + z
+            ae = 1.0
+            if ah[i] >= 0.0:
+                ae = min(ae, P[n1 * L + z]); ae = min(ae, M[n2 * L + z])
+            else:
+                ae = min(ae, M[n1 * L + z]); ae = min(ae, P[n2 * L + z])
+            ah2[i] = (1.0 - ae) * ah[i]
+            ah[i] = ae * ah[i]
+    for n in range(m.N):
+        for z in range(int(m.nlev_nod[n]) - 1):
+            LO[n * L + z] = LO[n * L + z] + (av[n * nl + z] - av[n * nl + z + 1]) * dt / area[n * nl + z] / hnn[n * L + z]
+    for e in range(m.E):
+        n1, n2 = ed[e]
+        for z in range(lev[e]):
+            LO[n1 * L + z] = LO[n1 * L + z] + ah[e * L + z] * dt / area[n1 * nl + z] / hnn[n1 * L + z]
+            LO[n2 * L + z] = LO[n2 * L + z] - ah[e * L + z] * dt / area[n2 * nl + z] / hnn[n2 * L + z]
+    return dict(LO=np.array(LO), adf_v=np.array(av2), adf_h=np.array(ah2), adf_v2=np.array(av2), adf_h2=np.array(ah2))
+
+
+def test_oracle_iter_yn_matches_fortran_transcription():
+    """The C restatement of the iter_yn branch (oracle_b3v/b3h with adf2, oracle_lo_update) against
+    a line-by-line Python transcription of the Fortran; nonzero initial adf_v2/adf_h2 check that
+    unassigned levels are carried through the whole-array swap."""
+    m = synth.config_mesh("tiny")
+    f = synth.make_fields(m)
+    st, p1 = O.pre_comm(m, f)
+    assert st == 5
+    rng = np.random.default_rng(11)
+    v2, h2 = rng.standard_normal(f["adf_v"].size), rng.standard_normal(f["adf_h"].size)
+    got = O.post_comm_iter(m, f, p1["plus"], p1["minus"], v2, h2)
+    want = _fortran_iter_phase2(m, f, p1["plus"], p1["minus"], v2, h2)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+    assert not np.array_equal(got["LO"], f["LO"])
+
+
+def test_iterated_pass_with_one_iteration_is_the_plain_pass():
+    m = synth.config_mesh("tiny")
+    f = synth.make_fields(m)
+    a, b = O.full_pass(m, f), O.iterated_pass(m, f, 1)
+    for k in ("adf_v", "adf_h", "del_v", "del_h"):
+        assert np.array_equal(a[k], b[k])
