@@ -86,13 +86,19 @@ def kernel_bytes(s, ntr=1):
 
 # ----------------------------------------------------------------------------- workload
 
-def build_local(args, rank, world):
+def global_dims(args, world):
+    """Global mesh: weak scaling stacks `world` copies of the config along y (1.2M nodes per GPU:
+    1600 x 6000 = 9.6M at 8 GPUs), strong scaling splits the config itself."""
     nx, ny, nl = synth.CONFIGS[args.config]
-    g = synth.make_mesh(nx, ny * world, nl, full_depth=not args.parity_levels,
-                        name=f"{args.config} x {world}")
+    return (nx, ny * world, nl) if args.scaling == "weak" else (nx, ny, nl)
+
+
+def build_local(args, rank, world):
+    nx, ny, nl = global_dims(args, world)
+    g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels, name=f"{args.config} x {world}")
     if world == 1:
         return g, None
-    part = partition.strip_parts(nx, ny * world, world)
+    part = partition.strip_parts(nx, ny, world)
     return partition.local_mesh(g, part, rank)  # (local mesh, halo lists)
 
 
@@ -122,8 +128,8 @@ def verify(args, e, step, m, fields, rank, world, dist):
         return None
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    nx, ny, nl = synth.CONFIGS[args.config]
-    g = synth.make_mesh(nx, ny * world, nl, full_depth=not args.parity_levels)
+    nx, ny, nl = global_dims(args, world)
+    g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels)
     wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
     bad = {}
     for k, fk in enumerate(synth.make_tracer_fields(g, ntr)):
@@ -151,7 +157,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="1.2M x 80", choices=list(synth.CONFIGS))
+    ap.add_argument("--config", default=None, choices=list(synth.CONFIGS),
+                    help="default: 1.2M x 80 per GPU (weak), 9.6M x 80 in total (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: the config per GPU; strong: the config split over the GPUs (SURVEY.md 8(e))")
     ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
@@ -164,6 +173,8 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "1.2M x 80" if args.scaling == "weak" else "9.6M x 80"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,7 +201,7 @@ def main():
     abi.set_path(args.path)
     dm = engine.DeviceMesh(m)
     dm.prepare()
-    e = engine.FctAle(dm, f) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
+    e = engine.FctAle(dm, f, copy=False) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
     stream = e.stream
 
     halo = None
@@ -309,13 +320,15 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "cell-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
-            "config": {"workload": f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}, "
-                                   f"{args.tracers} tracer{'s' if args.tracers > 1 else ''} per GPU"
+            "config": {"workload": f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}"
+                                   + (" per GPU" if args.scaling == "weak" else f" split over {world} GPU(s)")
+                                   + f", {args.tracers} tracer{'s' if args.tracers > 1 else ''}"
                                    + (" (batched)" if args.tracers > 1 else ""),
                        "tracers": args.tracers,
-                       "nodes_per_gpu": m.N, "levels": m.L, "global_nodes": m.N * world if world > 1 else m.N,
+                       "nodes_per_gpu": m.N, "levels": m.L,
+                       "global_nodes": global_dims(args, world)[0] * global_dims(args, world)[1],
                        "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
                        "parallelism": f"node partition y-strips x{world}, RCCL halo" if world > 1 else "1 GPU",
                        "path": args.path},

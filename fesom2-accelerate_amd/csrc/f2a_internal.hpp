@@ -174,8 +174,9 @@ hipError_t launch_cv(int n_owned, int nl, const int *nlev_nod, const real *ttf, 
 hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const real *area,
                      real *del_h, real dt, hipStream_t s);
 
-// Halo pack / unpack of (plus, minus) columns of ntr tracers (`stride` elements apart); the buffer
-// holds [list position][tracer][plus L | minus L], so each neighbour's part stays contiguous.
+// Halo pack / unpack of the columns of one or two (L, nodes) fields (`minus` may be null) of ntr
+// tracers (`stride` elements apart); the buffer holds [list position][tracer][field L (| field L)],
+// so each neighbour's part stays contiguous.
 hipError_t launch_halo_pack(const int *nodes, int count, int L, int ntr, size_t stride, const real *plus,
                             const real *minus, real *buf, hipStream_t s);
 hipError_t launch_halo_unpack(const int *nodes, int count, int L, int ntr, size_t stride, const real *buf,

@@ -1090,35 +1090,36 @@ static inline int levels_per_thread(int L)
 
 // ============================================================================ halo pack / unpack
 
+// halo buffers: [list position][tracer][field a L | field b L] (field b optional)
 __global__ __launch_bounds__(kBlock) void k_pack(const int *__restrict__ nodes, int count, int L,
                                                  int ntr, size_t stride,
-                                                 const real *__restrict__ plus,
-                                                 const real *__restrict__ minus,
+                                                 const real *__restrict__ fa,
+                                                 const real *__restrict__ fb,
                                                  real *__restrict__ buf)
 {
     const int i = wave_item();  // list position * ntr + tracer
     if (i >= count * ntr) return;
-    const int c = i / ntr, tr = i - c * ntr;
-    const size_t src = tr * stride + (size_t)nodes[c] * L, dst = (size_t)i * 2 * L;
+    const int c = i / ntr, tr = i - c * ntr, nf = fb ? 2 : 1;
+    const size_t src = tr * stride + (size_t)nodes[c] * L, dst = (size_t)i * nf * L;
     for (int z = threadIdx.x & 63; z < L; z += kWave) {
-        buf[dst + z] = plus[src + z];
-        buf[dst + L + z] = minus[src + z];
+        buf[dst + z] = fa[src + z];
+        if (fb) buf[dst + L + z] = fb[src + z];
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_unpack(const int *__restrict__ nodes, int count, int L,
                                                    int ntr, size_t stride,
                                                    const real *__restrict__ buf,
-                                                   real *__restrict__ plus,
-                                                   real *__restrict__ minus)
+                                                   real *__restrict__ fa,
+                                                   real *__restrict__ fb)
 {
     const int i = wave_item();
     if (i >= count * ntr) return;
-    const int c = i / ntr, tr = i - c * ntr;
-    const size_t dst = tr * stride + (size_t)nodes[c] * L, src = (size_t)i * 2 * L;
+    const int c = i / ntr, tr = i - c * ntr, nf = fb ? 2 : 1;
+    const size_t dst = tr * stride + (size_t)nodes[c] * L, src = (size_t)i * nf * L;
     for (int z = threadIdx.x & 63; z < L; z += kWave) {
-        plus[dst + z] = buf[src + z];
-        minus[dst + z] = buf[src + L + z];
+        fa[dst + z] = buf[src + z];
+        if (fb) fb[dst + z] = buf[src + L + z];
     }
 }
 

@@ -33,6 +33,12 @@ void set_mpi_rank_(int *rank, int *total_ranks)
 
 void transfer_mesh_(void **ret, int *host_ptr, int *size, int *istat)
 {
+    if (*size < 0) {
+        report("transfer_mesh_: size %d < 0", *size);
+        *ret = nullptr;
+        *istat = 1;
+        return;
+    }
     Buffer *m = allocate(host_ptr, (size_t)(*size) * sizeof(int), false);
     if (m && h2d(m, true, nullptr, false)) {
         *ret = m;
@@ -43,18 +49,39 @@ void transfer_mesh_(void **ret, int *host_ptr, int *size, int *istat)
     }
 }
 
-void alloc_var_(void **ret, real *host_ptr, int *size, bool *create_event, int *istat)
+static void alloc_doubles(void **ret, real *host_ptr, long long n, bool *create_event, int *istat, const char *who)
 {
-    Buffer *m = allocate(host_ptr, (size_t)(*size) * sizeof(real), create_event && *create_event);
+    *ret = nullptr;
+    *istat = 1;
+    if (n < 0) {
+        report("%s: size %lld < 0 (arrays of 2^31 or more doubles need fesom2_alloc_var_i8_)", who, n);
+        return;
+    }
+    Buffer *m = allocate(host_ptr, (size_t)n * sizeof(real), create_event && *create_event);
     *istat = m ? 0 : 1;
     *ret = m;
 }
 
+void alloc_var_(void **ret, real *host_ptr, int *size, bool *create_event, int *istat)
+{
+    alloc_doubles(ret, host_ptr, *size, create_event, istat, "alloc_var_");
+}
+
 void reserve_var_(void **ret, int *size, bool *create_event, int *istat)
 {
-    Buffer *m = allocate(nullptr, (size_t)(*size) * sizeof(real), create_event && *create_event);
-    *istat = m ? 0 : 1;
-    *ret = m;
+    alloc_doubles(ret, nullptr, *size, create_event, istat, "reserve_var_");
+}
+
+// 64-bit sizes: a whole 9.6M x 80 mesh on one GPU has 2.3e9-element fct_adf_h (the reference's
+// int size stops at 2^31-1)
+void fesom2_alloc_var_i8_(void **ret, real *host_ptr, long long *size, bool *create_event, int *istat)
+{
+    alloc_doubles(ret, host_ptr, *size, create_event, istat, "fesom2_alloc_var_i8_");
+}
+
+void fesom2_reserve_var_i8_(void **ret, long long *size, bool *create_event, int *istat)
+{
+    alloc_doubles(ret, nullptr, *size, create_event, istat, "fesom2_reserve_var_i8_");
 }
 
 void allocate_pinned_doubles_(void **hostptr, int *size, int *istat)

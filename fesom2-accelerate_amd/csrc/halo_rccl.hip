@@ -180,12 +180,13 @@ void fesom2_halo_plan_free_(void **plan)
 }  // extern "C"
 
 // pack -> grouped send/recv -> unpack, all on stream st (ntr tracers, `stride` doubles apart)
+// (bm may be null: one field)
 static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t stride, hipStream_t st)
 {
     if (!reserve_tracers(p, ntr)) return false;
-    const size_t w = 2 * (size_t)p->L * ntr;  // doubles per list position
-    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, ntr, stride, dptr<real>(bp), dptr<real>(bm), p->sbuf, st),
-            "halo pack"))
+    real *pa = dptr<real>(bp), *pb = bm ? dptr<real>(bm) : nullptr;
+    const size_t w = (bm ? 2 : 1) * (size_t)p->L * ntr;  // doubles per list position
+    if (!ok(launch_halo_pack(p->d_send, p->nsend, p->L, ntr, stride, pa, pb, p->sbuf, st), "halo pack"))
         return false;
     if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return false;
     for (size_t k = 0; k < p->ranks.size(); k++) {
@@ -201,8 +202,7 @@ static bool exchange_on(Comm *c, HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, s
         }
     }
     if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd")) return false;
-    return ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, ntr, stride, p->rbuf, dptr<real>(bp), dptr<real>(bm), st),
-              "halo unpack");
+    return ok(launch_halo_unpack(p->d_recv, p->nrecv, p->L, ntr, stride, p->rbuf, pa, pb, st), "halo unpack");
 }
 
 static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t stride)
@@ -213,8 +213,8 @@ static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t s
     }
     const size_t need_bytes = sizeof(real) * (stride * (ntr - 1)) + col_bytes(p->max_col + 1, p->L);
     for (Buffer *b : {bp, bm})
-        if (b->size < need_bytes) {
-            report("fct_plus/fct_minus holds %zu bytes, the halo plan needs %zu", b->size, need_bytes);
+        if (b && b->size < need_bytes) {
+            report("a field of the exchange holds %zu bytes, the halo plan needs %zu", b->size, need_bytes);
             return false;
         }
     return true;
@@ -265,6 +265,23 @@ void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **pla
     const size_t stride = (size_t)(*nod_columns) * p->L;
     if (!check_buffers(p, bp, bm, *ntracers, stride)) return;
     if (exchange_on(c, p, bp, bm, *ntracers, stride, stream_of(s))) *istat = 0;
+}
+
+// FESOM's exchange_nod(a) / exchange_nod(a, b) for (nl-1, nod) fields on the device: ttf/fct_LO
+// before phase 1, del_ttf_* after the c-step, fct_LO between iter_yn iterations.
+// field_b may be a null handle (one field); ntracers blocks nod_columns*(nl-1) doubles apart.
+void fesom2_exchange_nod_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
+                             int *nod_columns, void **field_a, void **field_b)
+{
+    *istat = 1;
+    Comm *c = comm_of(comm);
+    HaloPlan *p = plan_of(plan);
+    Buffer *ba = buf(field_a, "field_a");
+    Buffer *bb = (field_b && *field_b) ? buf(field_b, "field_b") : nullptr;
+    if (!c || !p || !ba || (field_b && *field_b && !bb)) return;
+    const size_t stride = (size_t)(*nod_columns) * p->L;
+    if (!check_buffers(p, ba, bb, *ntracers, stride)) return;
+    if (exchange_on(c, p, ba, bb, *ntracers, stride, stream_of(s))) *istat = 0;
 }
 
 }  // extern "C"

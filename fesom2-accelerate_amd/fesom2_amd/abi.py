@@ -29,7 +29,8 @@ EXPORTS = (
     "fesom2_halo_plan_free_", "fct_ale_exchange_acc_", "fct_ale_exchange_post_comm_c_acc_",
     "fct_ale_pre_comm_batched_acc_", "fct_ale_post_comm_c_batched_acc_", "fct_ale_exchange_batched_acc_",
     "fct_ale_exchange_post_comm_c_batched_acc_", "fct_ale_post_comm_iter_acc_",
-    "fct_ale_post_comm_iter_batched_acc_",
+    "fct_ale_post_comm_iter_batched_acc_", "fesom2_exchange_nod_acc_",
+    "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_",
 )
 
 _dll = None
@@ -77,6 +78,27 @@ def check(istat, what):
     v = istat.value if hasattr(istat, "value") else istat
     if v != 0:
         raise HipError(f"{what} failed (istat={v}): {last_error()}")
+
+
+def alloc_var(h, a, create_event=False):
+    """alloc_var_ (int size), or fesom2_alloc_var_i8_ past 2^31-1 elements."""
+    st = C.c_int(0)
+    n = max(a.size, 1)
+    if n < 2**31:
+        dll().alloc_var_(h.ref, arr(a), ip(n), bp(create_event), C.byref(st))
+    else:
+        dll().fesom2_alloc_var_i8_(h.ref, arr(a), C.byref(C.c_longlong(n)), bp(create_event), C.byref(st))
+    return st
+
+
+def reserve_var(h, n, create_event=False):
+    st = C.c_int(0)
+    n = max(n, 1)
+    if n < 2**31:
+        dll().reserve_var_(h.ref, ip(n), bp(create_event), C.byref(st))
+    else:
+        dll().fesom2_reserve_var_i8_(h.ref, C.byref(C.c_longlong(n)), bp(create_event), C.byref(st))
+    return st
 
 
 class Handle:

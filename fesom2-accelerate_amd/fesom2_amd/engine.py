@@ -68,13 +68,15 @@ class FctAle:
     """
 
     def __init__(self, dmesh: DeviceMesh, fields, stream=None, vlimit=1, flux_eps=1e-16, bignumber=1e3,
-                 dt=1.0):
+                 dt=1.0, copy=True):
         m = dmesh.m
         self.dm, self.m = dmesh, m
         self.stream = stream or abi.Stream()
         self.vlimit, self.eps, self.big, self.dt = vlimit, flux_eps, bignumber, dt
         NT, L, nl = m.N + m.H, m.L, m.nl
-        self.host = {k: np.ascontiguousarray(v, dtype=np.float64).copy() for k, v in fields.items()}
+        # copy=False binds the caller's arrays (large meshes: no second host copy)
+        self.host = {k: (np.array(v, dtype=np.float64) if copy else np.ascontiguousarray(v, dtype=np.float64))
+                     for k, v in fields.items()}
         self.host.setdefault("plus", np.zeros(NT * L))
         self.host.setdefault("minus", np.zeros(NT * L))
         self.h = {}
@@ -86,16 +88,12 @@ class FctAle:
             a = self.host[name]
             assert a.size == n, (name, a.size, n)
             h = abi.Handle(name)
-            st = C.c_int(0)
-            dll().alloc_var_(h.ref, arr(a), ip(n), bp(name in events), C.byref(st))
-            check(st, f"alloc_var_({name})")
+            check(abi.alloc_var(h, a, name in events), f"alloc_var_({name})")
             self.h[name] = h
             dll().transfer_var_(h.ref, arr(a))
         for name, n in (("ttf_max", NT * L), ("ttf_min", NT * L), ("UV_rhs", 2 * L * m.T)):
             h = abi.Handle(name)
-            st = C.c_int(0)
-            dll().reserve_var_(h.ref, ip(max(n, 1)), bp(False), C.byref(st))
-            check(st, f"reserve_var_({name})")
+            check(abi.reserve_var(h, n), f"reserve_var_({name})")
             self.h[name] = h
 
     # ------------------------------------------------------------------ phases (reference names)
@@ -151,9 +149,7 @@ class FctAle:
                 a = np.zeros_like(self.host[like])
                 self.host[name] = a
                 h = abi.Handle(name)
-                st = C.c_int(0)
-                dll().alloc_var_(h.ref, arr(a), ip(a.size), bp(False), C.byref(st))
-                check(st, f"alloc_var_({name})")
+                check(abi.alloc_var(h, a), f"alloc_var_({name})")
                 dll().transfer_var_(h.ref, arr(a))
                 self.h[name] = h
 
@@ -267,9 +263,7 @@ class FctAleBatch(FctAle):
         events = {"ttf", "adf_v", "adf_h"}
         for name, a in self.host.items():
             h = abi.Handle(name)
-            st = C.c_int(0)
-            dll().alloc_var_(h.ref, arr(a), ip(a.size), bp(name in events), C.byref(st))
-            check(st, f"alloc_var_({name})")
+            check(abi.alloc_var(h, a, name in events), f"alloc_var_({name})")
             self.h[name] = h
             dll().transfer_var_(h.ref, arr(a))
 

@@ -118,6 +118,12 @@ void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **
                               void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
                               real_type *dt);
 
+/* alloc_var_ / reserve_var_ with 64-bit element counts (a 9.6M-node x 80-level mesh on one GPU has
+ * 2.3e9-element fct_adf_h; the reference's int size stops at 2^31-1, and a negative int size is
+ * rejected with istat = 1). */
+void fesom2_alloc_var_i8_(void **ret, real_type *host_ptr, long long *size, bool *create_event, int *istat);
+void fesom2_reserve_var_i8_(void **ret, long long *size, bool *create_event, int *istat);
+
 /* Transfer mode.  0 (default) = reference semantics: pre_comm uploads fct_LO and downloads
  * fct_plus/minus, inter_comm downloads fct_adf_v, post_comm uploads fct_plus/minus and downloads
  * fct_adf_h, c downloads del_ttf_*.  1 = device resident: no implicit host transfers. */
@@ -208,6 +214,11 @@ void fct_ale_post_comm_c_batched_acc_(int *alg_state, void **s, int *ntracers, v
 /* nod_columns = myDim_nod2D + eDim_nod2D (the per-tracer stride in columns). */
 void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
                                    int *nod_columns, void **fct_plus, void **fct_minus);
+/* FESOM's exchange_nod(a) / exchange_nod(a, b) on the device for (nl-1, nod) fields -- ttf and
+ * fct_LO before phase 1, del_ttf_* after the c-step, fct_LO between iter_yn iterations
+ * (SURVEY.md 8(f) 3).  *field_b may be NULL (one field); ntracers blocks nod_columns*(nl-1) apart. */
+void fesom2_exchange_nod_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
+                             int *nod_columns, void **field_a, void **field_b);
 void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **comm, void **halo_plan,
                                                int *ntracers, void **fct_plus, void **fct_minus,
                                                void **fct_adf_v, void **fct_adf_h, void **del_ttf_advvert,

@@ -175,3 +175,35 @@ def test_overlapped_exchange_post_comm_c(comm, kind):
     for k in ("del_v", "del_h"):
         assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r][k], g.L, g.N), want[k]), k
     assert np.array_equal(partition.gather_owned(ms, lambda r: outs[r]["adf_v"], g.nl, g.N), want["adf_v"])
+
+
+@pytest.mark.parametrize("two", [False, True])
+@pytest.mark.parametrize("ntr", [1, 3])
+def test_exchange_nod_generic_fields(comm, two, ntr):
+    """fesom2_exchange_nod_acc_: FESOM's exchange_nod for one or two (nl-1, nod) fields of ntr
+    tracer blocks (ttf/LO before phase 1, del_ttf after c)."""
+    L, ncol = 12, 30
+    rng = np.random.default_rng(ntr + 10 * two)
+    fa, fb = rng.standard_normal(ntr * ncol * L), rng.standard_normal(ntr * ncol * L)
+    ha, hb = make_buffer(fa), make_buffer(fb)
+    plan, st = make_plan([0], [[2, 4, 6]], [[28, 29, 30]], L + 1)
+    assert st == 0
+    s = abi.Stream()
+    null = abi.Handle("none")
+    try:
+        ist = C.c_int(-1)
+        dll().fesom2_exchange_nod_acc_(C.byref(ist), s.ref, comm.ref, plan.ref, ip(ntr), ip(ncol), ha.ref,
+                                       hb.ref if two else null.ref)
+        assert ist.value == 0, abi.last_error()
+        s.sync()
+        for h, f0, moved in ((ha, fa, True), (hb, fb, two)):
+            got = download(h, f0.size).reshape(ntr, ncol, L)
+            want = f0.reshape(ntr, ncol, L).copy()
+            if moved:
+                want[:, [27, 28, 29]] = want[:, [1, 3, 5]]
+            assert np.array_equal(got, want)
+    finally:
+        dll().fesom2_halo_plan_free_(plan.ref)
+        dll().fesom2_free_(ha.ref)
+        dll().fesom2_free_(hb.ref)
+        s.free()

@@ -367,3 +367,23 @@ def test_iter_yn_whole_array_swap_keeps_unassigned_levels():
     finally:
         e.free()
         dm.free()
+
+
+def test_sizes_beyond_int32():
+    """The reference's int sizes stop at 2^31-1: a negative size is rejected (istat 1, no huge
+    hipMalloc), and the int64 entries allocate the same kind of handle."""
+    import ctypes as C
+    from fesom2_amd.abi import arr, bp, dll, ip
+    h = abi.Handle("neg")
+    st = C.c_int(0)
+    dll().alloc_var_(h.ref, None, ip(-5), bp(False), C.byref(st))
+    assert st.value == 1 and not h and "< 0" in abi.last_error()
+    a = np.arange(1000, dtype=np.float64)
+    h8 = abi.Handle("i8")
+    dll().fesom2_alloc_var_i8_(h8.ref, arr(a), C.byref(C.c_longlong(a.size)), bp(True), C.byref(st))
+    assert st.value == 0 and h8
+    dll().transfer_var_(h8.ref, arr(a))
+    out = np.zeros_like(a)
+    dll().fesom2_download_(h8.ref, arr(out), C.byref(st))
+    assert st.value == 0 and np.array_equal(out, a)
+    dll().fesom2_free_(h8.ref)
