@@ -79,9 +79,12 @@ def kernel_bytes(s, ntr=1):
     # p2: plus, minus, adf_v (r + w), del_v (r + w), del_h (r + w), ttf, LO, adf_h; area, hnode,
     # hnode_new shared
     p2 = ntr * 8 * (9 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
+    # p2 with b3h folded in: p2 + the limited adf_h written once (the other endpoint's plus/minus
+    # columns are re-reads of arrays p2 already reads)
+    p2f = p2 + ntr * 8 * ce
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
-    return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "pass": p1 + b3h + p2,
-            "survey_pass": survey}
+    return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
+            "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "survey_pass": survey}
 
 
 # ----------------------------------------------------------------------------- workload

@@ -78,6 +78,16 @@ Buffer *buf(void **h, const char *name)
     return b;
 }
 
+int *plan_edge_counters(const Plan *p, int ntr)
+{
+    if (ntr > p->cnt_tracers) {
+        p->edge_cnt = static_cast<int *>(p->cnt_mem.alloc(sizeof(int) * (size_t)std::max(p->dev.n_edges, 1) * ntr));
+        if (!p->edge_cnt) return nullptr;
+        p->cnt_tracers = ntr;
+    }
+    return p->edge_cnt;
+}
+
 Buffer *need(void **h, size_t bytes, const char *name)
 {
     Buffer *b = buf(h, name);
@@ -308,11 +318,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
             if (n1 < n_csr) {
                 other[pos[n1]] = n2;
-                refs[pos[n1]++] = {e, lev[e] << 1};
+                refs[pos[n1]++] = {e, lev[e] << 1, n2};
             }
             if (n2 < n_csr) {
                 other[pos[n2]] = n1;
-                refs[pos[n2]++] = {e, (lev[e] << 1) | 1};
+                refs[pos[n2]++] = {e, (lev[e] << 1) | 1, n1};
             }
         }
     }
@@ -465,6 +475,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         std::vector<NodeRec> p2(recs);
         std::stable_partition(p2.begin(), p2.end(), [&](const NodeRec &r) { return interior_node[r.info.n] != 0; });
         d.n_p2_interior = (int)std::count(interior_node.begin(), interior_node.end(), (char)1);
+        for (int n = 0; n < n_owned; n++) d.max_degree = std::max(d.max_degree, ptr[n + 1] - ptr[n]);
         d.p2_rec = plan->mem.upload(p2);
         d.node_info = plan->mem.upload(info);
         d.p_edges = plan->mem.upload(pedges);

@@ -82,7 +82,13 @@ struct Plan {
     DeviceArrays mem;
     bool has_ring = false;
     int lmax_edges = 0;
+    // per-edge arrival counters of the fused b3h, grown to the largest tracer batch seen
+    mutable DeviceArrays cnt_mem;
+    mutable int *edge_cnt = nullptr;
+    mutable int cnt_tracers = 0;
 };
+// The plan's edge counters for ntr tracers (nullptr on allocation failure).
+int *plan_edge_counters(const Plan *p, int ntr);
 
 // Node->edge CSR for nodes [0, n_csr) in ascending edge order; clusters for [0, n_owned) when the
 // element connectivity is present.  Validates every index; returns nullptr with `err` set.

@@ -26,9 +26,10 @@ struct Buffer {
 // One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the
 // order in which the reference's edge loops touch the node: reference.cpp:406-425).
 struct EdgeRef {
-    int edge;  // 0-based local edge
-    int code;  // (lev << 1) | second: lev = max(nl1, nl2) levels the edge carries
-               // (reference.cpp:412-414); second = this node is edges(2,e)
+    int edge;   // 0-based local edge
+    int code;   // (lev << 1) | second: lev = max(nl1, nl2) levels the edge carries
+                // (reference.cpp:412-414); second = this node is edges(2,e)
+    int other;  // 0-based local node at the other end (owned if < myDim_nod2D)
 };
 
 // One node of a node's cluster (the union of the nodes of its adjacent elements).  `lev` is the
@@ -50,7 +51,7 @@ struct NodeInfo {
     int pad;
 };
 
-// NodeInfo plus the first kRecRing cluster and kRecEdge edge entries inline (160 bytes, 16-byte
+// NodeInfo plus the first kRecRing cluster and kRecEdge edge entries inline (192 bytes, 16-byte
 // aligned): a block loads its columns' records with one coalesced sweep into LDS, so the gathers
 // depend on a single global load instead of NodeInfo -> CSR -> gather.  Entries beyond the inline
 // capacity stay in the processing-order CSRs at [r0 + kRecRing, r1) / [e0 + kRecEdge, e1).
@@ -60,7 +61,7 @@ struct alignas(16) NodeRec {
     RingRef ring[kRecRing];
     EdgeRef edge[kRecEdge];
 };
-static_assert(sizeof(NodeRec) == 160, "NodeRec layout");
+static_assert(sizeof(NodeRec) == 192, "NodeRec layout");
 
 // Device-side view of the derived mesh structures of one (mesh, partition) pair.
 struct MeshPlanDev {
@@ -89,6 +90,8 @@ struct MeshPlanDev {
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
     int n_p2_interior = 0;
+    int max_degree = 0;                   // most edges at one owned node
+    int *edge_cnt = nullptr;              // [n_edges * tracers] arrival counters of the fused b3h
 };
 
 // Batched tracers: `n` tracers whose per-tracer arrays follow each other in one buffer, `node`
@@ -120,8 +123,16 @@ struct P2Args {
     real *adf_v, *adf_h, *del_v, *del_h;
     real dt;
     Tracers tr;
+    int n_owned = 0;          // fused b3h (edge_cnt set): owned-node bound for `other`
+    int *edge_cnt = nullptr;  // fused b3h: zeroed per-edge(-per-tracer) arrival counters
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
+// b3-horizontal folded into the node kernel (a.edge_cnt zeroed, mp.max_degree <= kMaxFusedDegree):
+// every endpoint limits its edges' fluxes itself for c-horizontal, and the endpoint that arrives
+// last at an edge's counter -- after its block has read the raw column -- writes the limited
+// fct_adf_h.
+constexpr int kMaxFusedDegree = 32;
+hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);

@@ -37,7 +37,8 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 // residue class a contiguous range of tiles.  Speed only, never correctness.
 __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements)
 // FESOM2_ABLATE (timing-only builds of an experiment, results are wrong): bit 0 skips the cluster
-// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2.
+// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2, bit 3 the arrival
+// counters of the fused b3h.
 __constant__ int c_ablate = 0;
 // FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile order
 __constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
@@ -577,7 +578,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
         int code[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            const EdgeRef er = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0};
+            const EdgeRef er = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
             idx[k] = (size_t)er.edge * L + z0;
             code[k] = er.code;
         }
@@ -913,6 +914,177 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     if (nw <= 0) return;
     stv_s<C, NT>(a.del_v + b, dv, nw);
     stv_s<C, NT>(a.del_h + b, dh, nw);
+}
+
+// Edge gathers with the b3-horizontal limiter applied in-thread: for kBatch edges at a time the raw
+// flux and the other endpoint's plus/minus are loaded, then f(c, limited flux, second) runs in
+// ascending edge order.  (pn, mn: this node's plus/minus at the thread's levels.)
+template <int C, int kBatch, class F>
+__device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                                  const real *__restrict__ adf_h,
+                                                  const real *__restrict__ plus,
+                                                  const real *__restrict__ minus, const real (&pn)[C],
+                                                  const real (&mn)[C], int z0, int L, F &&f)
+{
+    for (int k0 = e0; k0 < e1; k0 += kBatch) {
+        EdgeRef er[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) er[k] = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
+        real h[kBatch][C], po[kBatch][C], mo[kBatch][C];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < (er[k].code >> 1)) {
+                ldv<C>(adf_h + (size_t)er[k].edge * L + z0, h[k]);
+                ldv<C>(plus + (size_t)er[k].other * L + z0, po[k]);
+                ldv<C>(minus + (size_t)er[k].other * L + z0, mo[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const int lev = er[k].code >> 1, second = er[k].code & 1;
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                if (z0 + c >= lev) continue;
+                // docs/refactoring.md:246-257 with (n1, n2) = (other, this) when second
+                const real ae = second ? b3h_factor(h[k][c], po[k][c], mo[k][c], pn[c], mn[c])
+                                       : b3h_factor(h[k][c], pn[c], mn[c], po[k][c], mo[k][c]);
+                f(c, ae * h[k][c], second);
+            }
+        }
+    }
+}
+
+// Phase 2 with b3-horizontal folded in (b3h + b3v + cv + ch, see launch_p2_fused_b3h).  Each
+// endpoint limits its edges' raw fluxes for its own c-horizontal; after the block barrier (every
+// raw fct_adf_h read of the block done) one thread per (column, edge) bumps the edge's counter, and
+// the endpoint that arrives last -- or the only owned one -- stores the limited column.
+template <int C, int KB>
+__global__ __launch_bounds__(1024) void k_p2f(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G] | writer masks[G]
+    const int L = a.nl - 1, S = L / C;
+    const int t = threadIdx.x;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.del_v += tr * a.tr.node;
+        a.del_h += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+        a.edge_cnt += (size_t)tr * mp.n_edges;
+    }
+    unsigned *wmask = reinterpret_cast<unsigned *>(reinterpret_cast<NodeRec *>(lds) + G);
+    if (t < G) wmask[t] = 0u;
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int Ln = ni.Ln;
+    const int top = Ln > 1 ? Ln : 1;
+    const int na = col ? max(0, min(C, top - z0)) : 0;
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;
+    const int ne = col ? ni.e1 - ni.e0 : 0;
+    real l[C], dv[C], dh[C], pn[C], mn[C];
+    size_t b = 0, ab = 0;
+    if (na > 0) {
+        b = (size_t)ni.n * L + z0;
+        ab = (size_t)ni.n * a.nl + z0;
+        real pp[C + 2], mm[C + 2], f[C + 1];
+        pp[0] = z0 ? a.plus[b - 1] : 0.;
+        mm[0] = z0 ? a.minus[b - 1] : 0.;
+        ldv<C>(a.plus + b, pn);
+        ldv<C>(a.minus + b, mn);
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            pp[c + 1] = pn[c];
+            mm[c + 1] = mn[c];
+        }
+        const bool below = z0 + C < Ln;
+        pp[C + 1] = below ? a.plus[b + C] : 0.;
+        mm[C + 1] = below ? a.minus[b + C] : 0.;
+#pragma unroll
+        for (int c = 0; c <= C; c++) f[c] = a.adf_v[ab + c];
+        real lim[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) {
+            const int z = z0 + c;
+            const bool lim_here = (c < C) ? (z < top) : (z < Ln);
+            lim[c] = lim_here ? b3v_factor(z, f[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) * f[c] : f[c];
+        }
+#pragma unroll
+        for (int c = 0; c < C; c++) l[c] = lim[c];
+        if (nw > 0) {
+            real del_v[C], ttf[C], hn[C], lo[C], hnn[C];
+            ldv<C>(a.del_v + b, del_v);
+            ldv<C>(a.ttf + b, ttf);
+            ldv<C>(a.hnode + b, hn);
+            ldv<C>(a.LO + b, lo);
+            ldv<C>(a.hnode_new + b, hnn);
+            ldv<C>(a.del_h + b, dh);
+            real dta[C];
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                dta[c] = c < nw ? a.dt / a.area[ab + c] : 0.;
+                real tv = del_v[c] - ttf[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
+                tv = tv + lo[c] * hnn[c];
+                dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
+            }
+            auto add = [&](int c, real h, int second) {
+                dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+            };
+            for_edges_limited<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L, add);
+            if (ne > kRecEdge)
+                for_edges_limited<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                         add);
+        }
+    }
+    __syncthreads();  // every raw fct_adf_v / fct_adf_h read of the block is done
+    if (c_ablate & 8) {  // timing only: static writer, no arrival counters (racy results)
+        for (int k = u; k < ne; k += S) {
+            const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+            if (!(er.code & 1)) atomicOr(&wmask[j], 1u << k);
+        }
+    } else {
+        for (int k = u; k < ne; k += S) {
+            const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+            if (er.other >= a.n_owned || atomicAdd(a.edge_cnt + er.edge, 1) == 1) atomicOr(&wmask[j], 1u << k);
+        }
+    }
+    __syncthreads();
+    if (na <= 0) return;
+#pragma unroll
+    for (int c = 0; c < C; c++)
+        if (c < na) a.adf_v[ab + c] = l[c];
+    if (nw <= 0) return;
+    stv<C>(a.del_v + b, dv, nw);
+    stv<C>(a.del_h + b, dh, nw);
+    const unsigned mine = wmask[j];
+    for (int k = 0; k < ne; k++) {
+        if (!((mine >> k) & 1u)) continue;
+        const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+        const int lev = er.code >> 1, second = er.code & 1;
+        if (z0 >= lev) continue;
+        real h[C], po[C], mo[C], out[C];
+        const size_t ie = (size_t)er.edge * L + z0;
+        ldv<C>(a.adf_h + ie, h);
+        ldv<C>(a.plus + (size_t)er.other * L + z0, po);
+        ldv<C>(a.minus + (size_t)er.other * L + z0, mo);
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            const real ae = second ? b3h_factor(h[c], po[c], mo[c], pn[c], mn[c])
+                                   : b3h_factor(h[c], pn[c], mn[c], po[c], mo[c]);
+            out[c] = ae * h[c];
+        }
+        stv<C>(a.adf_h + ie, out, min(C, lev - z0));
+    }
 }
 
 // iter_yn phase 2, nodes (see P2IterArgs).  Every slot of a column also copies fct_adf_v2 into
@@ -1301,6 +1473,21 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
         F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
     }
     F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+}
+
+hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * (sizeof(NodeRec) + sizeof(unsigned));
+    const int KB = env_int("FESOM2_P2F_BATCH", 2);
+    if (C == 2) {
+        if (KB == 4) F2A_LAUNCH_GROUPS((k_p2f<2, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 1) F2A_LAUNCH_GROUPS((k_p2f<2, 1>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2f<2, 2>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    F2A_LAUNCH_GROUPS((k_p2f<1, 2>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)

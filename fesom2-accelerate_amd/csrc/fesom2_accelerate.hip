@@ -413,21 +413,40 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                   dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
-    if (!run("fct_ale_b3_horizontal", st, [&] {
-            return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
-        }))
-        return;
-    if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
-    if (comm) {
-        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
-        if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
-                return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
-                                             dptr<real>(badfh), a.tr, st);
+    // b3-horizontal folded into the node kernel (default), or its own edge kernel first
+    // (FESOM2_FUSE_B3H=0, or a node with more than kMaxFusedDegree edges)
+    const char *fuse_s = getenv("FESOM2_FUSE_B3H");
+    const int fuse_env = fuse_s ? atoi(fuse_s) : 0;  // measured slower: opt-in
+    const bool fuse = fuse_env != 0 && d.max_degree <= f2a::kMaxFusedDegree;
+    if (fuse) {
+        a.n_owned = N;
+        a.edge_cnt = plan_edge_counters(plan, ntr);
+        if (!a.edge_cnt ||
+            !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
+            return;
+        if (!run("fct_ale_p2_b3h", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
+    } else {
+        if (!run("fct_ale_b3_horizontal", st, [&] {
+                return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
+                                             a.tr, st);
             }))
             return;
+        if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
+    }
+    if (comm) {
+        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
         a.nodes = d.p2_rec + n_first;
         a.count = N - n_first;
-        if (!run("fct_ale_p2_boundary", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
+        if (fuse) {
+            if (!run("fct_ale_p2_b3h_boundary", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
+        } else {
+            if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
+                    return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
+                                                 dptr<real>(badfh), a.tr, st);
+                }))
+                return;
+            if (!run("fct_ale_p2_boundary", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
+        }
     }
     *alg_state = 9;
     if (!g_resident)

@@ -19,7 +19,8 @@ import csv
 import json
 import sys
 
-NAMES = {"k_p1": "fct_ale_p1", "k_p2": "fct_ale_p2", "k_b3h_g": "fct_ale_b3_horizontal"}
+NAMES = {"k_p1": "fct_ale_p1", "k_p2": "fct_ale_p2", "k_b3h_g": "fct_ale_b3_horizontal",
+         "k_b3h_u": "fct_ale_b3_horizontal", "k_p2f": "fct_ale_p2_b3h"}
 
 
 def per_kernel(path):
