@@ -373,6 +373,35 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             zdry[n] = zd;
             rptr[n + 1] = (int)ring.size();
         }
+        // does every owned node's cluster equal {n} + its edge neighbours, on the edges' levels?
+        if (n_csr >= n_owned) {
+            bool same = true;
+            for (int n = 0; n < n_owned && same; n++) {
+                const int ne = ptr[n + 1] - ptr[n], nr = rptr[n + 1] - rptr[n];
+                if (nr != ne + 1) {
+                    same = false;
+                    break;
+                }
+                int self = -1, emax = 0;
+                for (int k = ptr[n]; k < ptr[n + 1]; k++) emax = std::max(emax, refs[k].code >> 1);
+                for (int r = rptr[n]; r < rptr[n + 1] && same; r++) {
+                    const RingRef rr = ring[r];
+                    if (rr.node == n) {
+                        self = rr.lev;
+                        continue;
+                    }
+                    bool found = false;
+                    for (int k = ptr[n]; k < ptr[n + 1]; k++)
+                        if (refs[k].other == rr.node) {
+                            found = (refs[k].code >> 1) == rr.lev;
+                            break;
+                        }
+                    same = found;
+                }
+                same = same && self == emax;
+            }
+            d.edge_cluster = same;
+        }
         d.ring_ptr = plan->mem.upload(rptr);
         d.ring = plan->mem.upload(ring);
         d.zdry = plan->mem.upload(zdry);
@@ -440,7 +469,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             if (with_ring) pring.insert(pring.end(), ring.begin() + rptr[n], ring.begin() + rptr[n + 1]);
             ni.r1 = (int)pring.size();
             ni.zdry = with_ring ? zdry[n] : 0;
-            ni.pad = 0;
+            ni.self_lev = 0;
+            if (with_ring)
+                for (int r = rptr[n]; r < rptr[n + 1]; r++)
+                    if (ring[r].node == n) ni.self_lev = ring[r].lev;
         }
         // edges in the order of their first visited endpoint (edges without an owned endpoint last)
         std::vector<int4> einfo;
@@ -468,6 +500,45 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             for (int q = 0; q < kRecEdge && info[k].e0 + q < info[k].e1; q++) r.edge[q] = pedges[info[k].e0 + q];
         }
         d.node_rec = plan->mem.upload(recs);
+        // cluster staging plan for phase 1 (see MeshPlanDev::stage_*)
+        if (with_ring) {
+            const int SG = f2a::fused_group_columns(nl);
+            std::vector<int> bptr(1, 0), bnodes;
+            std::vector<NodeRec> srecs(recs);
+            std::vector<RingRef> sring(pring);
+            int umax = 0;
+            for (int b0 = 0; b0 < n_owned; b0 += SG) {
+                const int base = (int)bnodes.size();
+                auto slot = [&](int v) {
+                    for (int q = base; q < (int)bnodes.size(); q++)
+                        if (bnodes[q] == v) return q - base;
+                    bnodes.push_back(v);
+                    return (int)bnodes.size() - 1 - base;
+                };
+                for (int k = b0; k < std::min(b0 + SG, n_owned); k++)
+                    for (int r = info[k].r0; r < info[k].r1; r++) sring[r].node = slot(pring[r].node);
+                for (int k = b0; k < std::min(b0 + SG, n_owned); k++)
+                    for (int q = 0; q < kRecRing && info[k].r0 + q < info[k].r1; q++)
+                        srecs[k].ring[q] = sring[info[k].r0 + q];
+                umax = std::max(umax, (int)bnodes.size() - base);
+                bptr.push_back((int)bnodes.size());
+            }
+            if (getenv("FESOM2_PLAN_STATS"))
+                fprintf(stderr, "fesom2-accelerate: staging G=%d blocks=%zu union mean %.2f max %d, ring mean %.2f\n", SG,
+                        bptr.size() - 1, (double)bnodes.size() / std::max<size_t>(bptr.size() - 1, 1), umax,
+                        (double)pring.size() / std::max(n_owned, 1));
+            if (umax <= f2a::kMaxStage) {
+                d.stage_G = SG;
+                d.stage_max = umax;
+                d.blk_ptr = plan->mem.upload(bptr);
+                d.blk_nodes = plan->mem.upload(bnodes);
+                d.s_rec = plan->mem.upload(srecs);
+                d.s_ring = plan->mem.upload(sring);
+                if (!d.blk_ptr || !d.blk_nodes || !d.s_rec || !d.s_ring)
+                    return fail("device allocation for the staging plan failed");
+            }
+        }
+
         std::vector<char> interior_node(n_owned, 1);
         for (int n = 0; n < n_owned; n++)
             for (int k = ptr[n]; k < ptr[n + 1]; k++)

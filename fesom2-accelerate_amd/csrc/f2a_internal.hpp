@@ -48,7 +48,7 @@ struct NodeInfo {
     int r0, r1;
     int e0, e1;
     int zdry;  // min over adjacent elements of (nlevels(e) - 1); levels >= zdry see the a2 fill
-    int pad;
+    int self_lev;  // levels on which the node itself is in its cluster (max over its elements)
 };
 
 // NodeInfo plus the first kRecRing cluster and kRecEdge edge entries inline (192 bytes, 16-byte
@@ -91,6 +91,16 @@ struct MeshPlanDev {
     const NodeRec *p2_rec = nullptr;      // [n_owned]
     int n_p2_interior = 0;
     int max_degree = 0;                   // most edges at one owned node
+    // every owned node's cluster is the node plus its edge neighbours, each on its edge's levels
+    // (a consistent triangulation): phase 1 gathers ttf/LO along the edge list
+    bool edge_cluster = false;
+    // phase-1 cluster staging: for block b (stage_G consecutive positions) the distinct cluster
+    // nodes blk_nodes[blk_ptr[b] .. blk_ptr[b+1]) are staged into LDS once; s_rec / s_ring are
+    // node_rec / p_ring with every cluster node replaced by its slot in the block's list
+    int stage_G = 0, stage_max = 0;       // stage_max = 0: staging off (no ring, or unions too large)
+    const int *blk_ptr = nullptr, *blk_nodes = nullptr;
+    const NodeRec *s_rec = nullptr;
+    const RingRef *s_ring = nullptr;
     int *edge_cnt = nullptr;              // [n_edges * tracers] arrival counters of the fused b3h
 };
 
@@ -155,6 +165,9 @@ hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, cons
                            real *adf_h2, const Tracers &tr, hipStream_t s);
 // columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
 int group_columns(int L);
+// columns per block of the fused node kernels for nl levels (the staging plan's block size)
+int fused_group_columns(int nl);
+constexpr int kMaxStage = 64;  // most distinct cluster nodes a block stages
 
 // Stepwise kernels, one per reference step.
 hipError_t launch_a1(int n_nodes, int nl, const int *nlev_nod, const real *LO, const real *ttf,

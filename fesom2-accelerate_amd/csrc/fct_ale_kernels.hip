@@ -916,6 +916,324 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
+// Phase-1 edge loop that also gathers the cluster (MeshPlanDev::edge_cluster): per edge the raw
+// flux and the other endpoint's LO/ttf, kBatch edges at a time; b1-horizontal sums in ascending
+// edge order (f), max/min(LO, ttf) of the neighbour on the edge's levels into vx/vn.
+template <int C, int kBatch, class F>
+__device__ __forceinline__ void for_edges_cluster(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                                  const real *__restrict__ adf_h,
+                                                  const real *__restrict__ LO,
+                                                  const real *__restrict__ ttf, int z0, int L,
+                                                  real (&vx)[C], real (&vn)[C], F &&f)
+{
+    for (int k0 = e0; k0 < e1; k0 += kBatch) {
+        EdgeRef er[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) er[k] = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
+        real h[kBatch][C], lo[kBatch][C], tt[kBatch][C];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < (er[k].code >> 1)) {
+                ldv<C>(adf_h + (size_t)er[k].edge * L + z0, h[k]);
+                ldv<C>(LO + (size_t)er[k].other * L + z0, lo[k]);
+                ldv<C>(ttf + (size_t)er[k].other * L + z0, tt[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const int lev = er[k].code >> 1;
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                if (z0 + c < lev) {
+                    f(c, h[k][c], er[k].code & 1);
+                    vx[c] = RMAX(vx[c], RMAX(lo[k][c], tt[k][c]));
+                    vn[c] = RMIN(vn[c], RMIN(lo[k][c], tt[k][c]));
+                }
+        }
+    }
+}
+
+// Phase 1 with the cluster taken along the edge list (see for_edges_cluster): one gather loop of
+// three columns per edge instead of a cluster loop and an edge loop, and the node's own LO/ttf
+// loaded once for both its cluster term and b2.
+template <int VLIMIT, int C, int EB>
+__global__ __launch_bounds__(1024) void k_p1e(MeshPlanDev mp, P1Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
+    const int L = a.nl - 1, S = L / C;
+    const int t = threadIdx.x;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 1) * G;
+    if (tr) {
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
+    const int ncol = min(G, a.n_owned - first);
+    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int Ln = ni.Ln;
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;
+    real vx[C], vn[C], p[C], m[C], lo[C], tt[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = lo[c] = tt[c] = 0.;
+    size_t b = 0, ab = 0;
+    if (nw > 0) {
+        b = (size_t)ni.n * L + z0;
+        ab = (size_t)ni.n * a.nl + z0;
+        ldv<C>(a.LO + b, lo);
+        ldv<C>(a.ttf + b, tt);
+        real v[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? a.adf_v[ab + c] : 0.;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
+            m[c] = RMIN(0., v[c]) + RMIN(0., -v[c + 1]);
+            const bool dry = z0 + c >= ni.zdry;
+            vx[c] = dry ? -a.big : -INFINITY;
+            vn[c] = dry ? a.big : INFINITY;
+            if (z0 + c < ni.self_lev) {  // the node itself
+                vx[c] = RMAX(vx[c], RMAX(lo[c], tt[c]));
+                vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
+            }
+        }
+        const int ne = (c_ablate & 2) ? 0 : ni.e1 - ni.e0;
+        auto add = [&](int c, real h, int second) {
+            if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
+                p[c] += RMAX(0., -h);
+                m[c] += RMIN(0., -h);
+            } else {
+                p[c] += RMAX(0., h);
+                m[c] += RMIN(0., h);
+            }
+        };
+        for_edges_cluster<C, EB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.LO, a.ttf, z0, L, vx, vn, add);
+        if (ne > kRecEdge)
+            for_edges_cluster<C, EB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.LO, a.ttf, z0, L, vx, vn, add);
+    }
+    real *tvx = lds, *tvn = lds + G * L;
+    const int q = j * L + z0;
+    if (col) {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            tvx[q + c] = vx[c];
+            tvn[q + c] = vn[c];
+        }
+    }
+    __syncthreads();
+    if (nw == 0) return;
+    real ai[C], op[C], om[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        op[c] = om[c] = 0.;
+        const int z = z0 + c;
+        if (c >= nw) continue;
+        real tm, tn;
+        if (VLIMIT == 1) {
+            if (z == 0 || z == Ln - 1) {
+                tm = tvx[q + c];
+                tn = tvn[q + c];
+            } else {
+                tm = RMAX(RMAX(tvx[q + c - 1], tvx[q + c]), tvx[q + c + 1]);
+                tn = RMIN(RMIN(tvn[q + c - 1], tvn[q + c]), tvn[q + c + 1]);
+            }
+        } else {
+            tm = tvx[q + c];
+            tn = tvn[q + c];
+            if (z >= 1 && z < Ln - 1) {
+                const size_t bz = b + c;
+                const real c0 = RMAX(a.LO[bz - 1], a.ttf[bz - 1]);
+                const real c1 = RMAX(a.LO[bz], a.ttf[bz]);
+                const real c2 = RMAX(a.LO[bz + 1], a.ttf[bz + 1]);
+                const real hmx = RMAX(RMAX(c0, c1), c2);
+                const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
+                if (VLIMIT == 2) {
+                    tm = RMAX(tm, hmx);
+                    tn = RMIN(tn, hmn);
+                } else {
+                    tm = RMIN(tm, hmx);
+                    tn = RMAX(tn, hmn);
+                }
+            }
+        }
+        real flux = p[c] * a.dt * ai[c] + a.eps;  // b2, reference.cpp:432-435
+        op[c] = RMIN(1., (tm - lo[c]) / flux);
+        flux = m[c] * a.dt * ai[c] - a.eps;
+        om[c] = RMIN(1., (tn - lo[c]) / flux);
+    }
+    stv<C>(a.plus + b, op, nw);
+    stv<C>(a.minus + b, om, nw);
+}
+
+// cluster bound from the staged columns (slot = position in the block's cluster list)
+template <int C>
+__device__ __forceinline__ void cluster_bound_lds(const RingRef *__restrict__ ring, int r0, int r1,
+                                                  const real *smx, const real *smn, int z0, int L,
+                                                  real (&vx)[C], real (&vn)[C])
+{
+    for (int r = r0; r < r1; r++) {
+        const RingRef rr = ring[r];
+        const int q = rr.node * L + z0;
+#pragma unroll
+        for (int c = 0; c < C; c++)
+            if (z0 + c < rr.lev) {
+                vx[c] = RMAX(vx[c], smx[q + c]);
+                vn[c] = RMIN(vn[c], smn[q + c]);
+            }
+    }
+}
+
+// Phase 1 (vlimit 1) with the cluster staged: the block's distinct cluster columns (MeshPlanDev
+// stage_*) are read once, max/min(LO, ttf) per level go to LDS, and every column's tvert comes from
+// LDS -- one round of independent loads instead of a dependent gather batch per cluster member.
+// The tvert stencil arrays then reuse the staging area.
+template <int C, int EB, int KS>
+__global__ __launch_bounds__(1024) void k_p1s(MeshPlanDev mp, P1Args a, int G, float invS, int U)
+{
+    extern __shared__ real lds[];  // staged max | staged min (U*L each; later tvx | tvn) | NodeRec[G]
+    const int L = a.nl - 1, S = L / C;
+    const int t = threadIdx.x;
+    int tr;
+    const int grp = group_tracer(a.tr.n, tr, c_tracer_major & 1);
+    const int first = grp * G;
+    if (tr) {
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
+    const int ncol = min(G, a.n_owned - first);
+    real *smx = lds, *smn = lds + U * L;
+    const NodeRec *recs = stage_records(mp.s_rec, first, ncol, lds + 2 * U * L);
+    {
+        // every item's index and column loads are issued before any is consumed
+        const int u0 = mp.blk_ptr[grp], nitems = (mp.blk_ptr[grp + 1] - u0) * S;
+        const int nt = blockDim.x;
+        int dst[KS];
+        size_t src[KS];
+#pragma unroll
+        for (int k = 0; k < KS; k++) {
+            const int it = t + k * nt;
+            int q = 0, sl = 0;
+            if (it < nitems) slot_of(it, S, invS, q, sl);
+            dst[k] = it < nitems ? q * L + C * sl : -1;
+            src[k] = it < nitems ? (size_t)mp.blk_nodes[u0 + q] * L + C * sl : 0;
+        }
+        real lo[KS][C], tt[KS][C];
+#pragma unroll
+        for (int k = 0; k < KS; k++)
+            if (dst[k] >= 0) {
+                ldv<C>(a.LO + src[k], lo[k]);
+                ldv<C>(a.ttf + src[k], tt[k]);
+            }
+#pragma unroll
+        for (int k = 0; k < KS; k++)
+            if (dst[k] >= 0)
+#pragma unroll
+                for (int c = 0; c < C; c++) {
+                    smx[dst[k] + c] = RMAX(lo[k][c], tt[k][c]);
+                    smn[dst[k] + c] = RMIN(lo[k][c], tt[k][c]);
+                }
+    }
+    int j, u;
+    slot_of(t, S, invS, j, u);
+    const int z0 = C * u;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int Ln = ni.Ln;
+    const int nw = col ? max(0, min(C, Ln - z0)) : 0;
+    real vx[C], vn[C], p[C], m[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = 0.;
+    size_t b = 0, ab = 0;
+    if (nw > 0) {
+        b = (size_t)ni.n * L + z0;
+        ab = (size_t)ni.n * a.nl + z0;
+        real v[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? a.adf_v[ab + c] : 0.;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
+            m[c] = RMIN(0., v[c]) + RMIN(0., -v[c + 1]);
+        }
+        const int ne = ni.e1 - ni.e0;
+        auto add = [&](int c, real h, int second) {
+            if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
+                p[c] += RMAX(0., -h);
+                m[c] += RMIN(0., -h);
+            } else {
+                p[c] += RMAX(0., h);
+                m[c] += RMIN(0., h);
+            }
+        };
+        for_edges<C, EB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+        if (ne > kRecEdge) for_edges<C, EB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+    }
+    __syncthreads();  // staged columns complete
+    if (nw > 0) {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            const bool dry = z0 + c >= ni.zdry;
+            vx[c] = dry ? -a.big : -INFINITY;
+            vn[c] = dry ? a.big : INFINITY;
+        }
+        const int nr = ni.r1 - ni.r0;
+        cluster_bound_lds<C>(recs[j].ring, 0, min(nr, kRecRing), smx, smn, z0, L, vx, vn);
+        if (nr > kRecRing) cluster_bound_lds<C>(mp.s_ring, ni.r0 + kRecRing, ni.r1, smx, smn, z0, L, vx, vn);
+    }
+    __syncthreads();  // staging area free: tvert goes there
+    real *tvx = lds, *tvn = lds + G * L;
+    const int q = j * L + z0;
+    if (col) {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            tvx[q + c] = vx[c];
+            tvn[q + c] = vn[c];
+        }
+    }
+    __syncthreads();
+    if (nw == 0) return;
+    real lo[C], ai[C], op[C], om[C];
+    ldv<C>(a.LO + b, lo);
+#pragma unroll
+    for (int c = 0; c < C; c++) ai[c] = c < nw ? a.area_inv[ab + c] : 0.;
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        op[c] = om[c] = 0.;
+        const int z = z0 + c;
+        if (c >= nw) continue;
+        real tm, tn;
+        if (z == 0 || z == Ln - 1) {
+            tm = tvx[q + c];
+            tn = tvn[q + c];
+        } else {
+            tm = RMAX(RMAX(tvx[q + c - 1], tvx[q + c]), tvx[q + c + 1]);
+            tn = RMIN(RMIN(tvn[q + c - 1], tvn[q + c]), tvn[q + c + 1]);
+        }
+        real flux = p[c] * a.dt * ai[c] + a.eps;  // b2, reference.cpp:432-435
+        op[c] = RMIN(1., (tm - lo[c]) / flux);
+        flux = m[c] * a.dt * ai[c] - a.eps;
+        om[c] = RMIN(1., (tn - lo[c]) / flux);
+    }
+    stv<C>(a.plus + b, op, nw);
+    stv<C>(a.minus + b, om, nw);
+}
+
 // Edge gathers with the b3-horizontal limiter applied in-thread: for kBatch edges at a time the raw
 // flux and the other endpoint's plus/minus are loaded, then f(c, limited flux, second) runs in
 // ascending edge order.  (pn, mn: this node's plus/minus at the thread's levels.)
@@ -1247,6 +1565,14 @@ int group_columns(int S)
         }
         if (waste < 1.0 + 1e-9) break;
     }
+    // FESOM2_GROUP_SHIFT = k: 2^k times as many columns per block (k < 0: fewer; A/B measurements,
+    // results do not depend on it)
+    static const int shift = [] {
+        const char *e = getenv("FESOM2_GROUP_SHIFT");
+        return e ? atoi(e) : 0;
+    }();
+    for (int k = 0; k < shift && best * 2 * S <= 1024; k++) best *= 2;
+    for (int k = 0; k > shift && best > 1; k--) best /= 2;
     return best;
 }
 
@@ -1412,10 +1738,49 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
     F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
+int fused_group_columns(int nl)
+{
+    const int L = nl - 1;
+    return group_columns(L / levels_per_thread(L));
+}
+
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+    // cluster along the edge list (FESOM2_P1_EDGE=1 where the plan verified it; measured equal at
+    // EB = 1, slower at EB >= 2: DESIGN.md §3)
+    if (mp.edge_cluster && env_int("FESOM2_P1_EDGE", 0)) {
+        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+        const float invS = 1.0f / (float)S;
+        const int EB = env_int("FESOM2_P1E_EB", 2);
+#define F2A_P1E(CC, EBV)                                                                                        \
+        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1e<2, CC, EBV>), groups, G, S, lds, s, mp, a, G, invS);  \
+        if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1e<3, CC, EBV>), groups, G, S, lds, s, mp, a, G, invS);  \
+        F2A_LAUNCH_GROUPS((k_p1e<1, CC, EBV>), groups, G, S, lds, s, mp, a, G, invS);
+        if (C == 2) {
+            if (EB == 1) { F2A_P1E(2, 1) }
+            if (EB == 4) { F2A_P1E(2, 4) }
+            F2A_P1E(2, 2)
+        }
+        F2A_P1E(1, 2)
+#undef F2A_P1E
+    }
+    // staged cluster (FESOM2_P1_STAGE=1; vlimit 1 only; measured slower at G = 8)
+    if (a.vlimit == 1 && mp.stage_max > 0 && mp.stage_G == G && env_int("FESOM2_P1_STAGE", 0)) {
+        const int U = std::max(mp.stage_max, G);
+        const size_t lds = 2 * (size_t)U * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+        const float invS = 1.0f / (float)S;
+        const int EB = env_int("FESOM2_P1S_EB", 2);
+        const int KS = (mp.stage_max * S + (int)threads_for(G, S) - 1) / (int)threads_for(G, S);  // items per thread
+        if (C == 2 && KS <= 8) {
+#define F2A_P1S(EBV, KSV) \
+            if (EB == EBV && KS <= KSV) F2A_LAUNCH_GROUPS((k_p1s<2, EBV, KSV>), groups, G, S, lds, s, mp, a, G, invS, U);
+            F2A_P1S(2, 2) F2A_P1S(2, 4) F2A_P1S(2, 6) F2A_P1S(2, 8)
+            F2A_P1S(4, 2) F2A_P1S(4, 4) F2A_P1S(4, 6) F2A_P1S(4, 8)
+#undef F2A_P1S
+        }
+    }
     // batch sizes of the cluster / edge gathers (FESOM2_P1_BATCH = 10*RB + EB; measured)
     switch (env_int("FESOM2_P1_BATCH", 22)) {
     case 44: return C == 2 ? p1_launch<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch<1, 4, 4>(mp, a, s, G, S, groups);

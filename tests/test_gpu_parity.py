@@ -86,7 +86,10 @@ def test_full_pass_matches_oracle(name, full, perm, fused, path):
 KNOBS = [{"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "0"}, {"FESOM2_B3H_U": "4", "FESOM2_B3H_NT": "0"},
          {"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "1"}, {"FESOM2_B3H_CPT": "4"}, {"FESOM2_NT": "3"},
          {"FESOM2_P1_BATCH": "44", "FESOM2_P2_BATCH": "8"}, {"FESOM2_PATCH": "0"}, {"FESOM2_PATCH": "7"}, {"FESOM2_FUSE_B3H": "1"},
-         {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "1"}, {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "4"}]
+         {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "1"}, {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "4"},
+         {"FESOM2_P1_STAGE": "1", "FESOM2_P1_EDGE": "0"},
+         {"FESOM2_P1_STAGE": "1", "FESOM2_P1_EDGE": "0", "FESOM2_P1S_EB": "4"}, {"FESOM2_P1_EDGE": "0"},
+         {"FESOM2_P1E_EB": "1"}, {"FESOM2_P1E_EB": "4"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
