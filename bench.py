@@ -173,6 +173,9 @@ def main():
     ap.add_argument("--check", action="store_true",
                     help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
                          "oracle on the global mesh (gathered over ranks)")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
+                    help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "
+                         "over gloo (validation only: lets N ranks share one GPU, which RCCL refuses)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
     args = ap.parse_args()
@@ -192,7 +195,17 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        # gloo reports its connections on stdout; the driver reads rank 0's one JSON line there, so
+        # fd 1 goes to stderr while the group connects (for good on ranks other than 0)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
         dist.init_process_group("gloo")
+        dist.barrier()
+        sys.stdout.flush()
+        if rank == 0:
+            os.dup2(saved, 1)
+        os.close(saved)
 
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
@@ -208,7 +221,7 @@ def main():
     stream = e.stream
 
     halo = None
-    if world > 1:
+    if world > 1 and args.exchange == "rccl":
         import ctypes as C
         uid = engine.Halo.unique_id() if rank == 0 else (C.c_char * 128)()
         t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
@@ -218,11 +231,32 @@ def main():
         log(f"rank {rank}: owned {m.N} halo {m.H} neighbours {lists.neighbors} "
             f"send {[lists.send[q].size for q in lists.neighbors]} recv {[lists.recv[q].size for q in lists.neighbors]}")
 
+    def host_exchange():
+        """fct_plus/fct_minus halo through host memory and gloo (--exchange host)."""
+        abi.device_sync()
+        pm = [e.download(k).reshape(args.tracers, -1, m.L) for k in ("plus", "minus")]
+        ops, bufs = [], {}
+        for q in lists.neighbors:
+            out = np.ascontiguousarray(np.stack([a[:, lists.send[q] - 1] for a in pm]))
+            bufs[q] = np.empty((2, args.tracers, lists.recv[q].size, m.L))
+            ops.append(dist.P2POp(dist.isend, torch.from_numpy(out), q))
+            ops.append(dist.P2POp(dist.irecv, torch.from_numpy(bufs[q]), q))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for q in lists.neighbors:
+            for i, a in enumerate(pm):
+                a[:, lists.recv[q] - 1] = bufs[q][i]
+        e.upload("plus", pm[0].reshape(-1))
+        e.upload("minus", pm[1].reshape(-1))
+
     def step():
         s1 = e.pre_comm()
         if s1 != 6:
             raise RuntimeError(f"pre_comm alg_state {s1}: {abi.last_error()}")
-        if args.path == "stepwise":
+        if world > 1 and args.exchange == "host":
+            host_exchange()
+            s2 = e.post_comm_c() if args.path == "fused" else (e.inter_comm(), e.post_comm(), e.c_step())[-1]
+        elif args.path == "stepwise":
             if halo is not None:
                 e.exchange(halo.comm, halo.plan)
             s2 = (e.inter_comm(), e.post_comm(), e.c_step())[-1]
@@ -333,7 +367,10 @@ def main():
                        "nodes_per_gpu": m.N, "levels": m.L,
                        "global_nodes": global_dims(args, world)[0] * global_dims(args, world)[1],
                        "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
-                       "parallelism": f"node partition y-strips x{world}, RCCL halo" if world > 1 else "1 GPU",
+                       "parallelism": (f"node partition y-strips x{world}, "
+                                       + ("RCCL halo overlapped with interior phase 2" if args.exchange == "rccl"
+                                          else "host/gloo halo (validation, not a benchmark)"))
+                       if world > 1 else "1 GPU",
                        "path": args.path},
             "roofline": roof,
             "cpu_baseline": cpu,
