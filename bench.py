@@ -17,7 +17,9 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 * roofline  the dominant kernel's algorithmic bytes per launch / its average launch time (HIP events
             on its stream, recorded inside the library around every launch), against 8.0 TB/s.
 * cpu_baseline  the oracle's single-threaded full pass (bit-identical to reference.cpp for a1..b2)
-            on the same mesh, rank 0 at N = 1 only.
+            on the same mesh, rank 0 at N = 1 only; plus "all_cores": P single-threaded oracle
+            processes on a P-way strip partition of the same mesh (MPI-style replicas, SURVEY.md
+            8(d)), run before this process touches the GPU.
 
 Loads the engine library before torch so the process runs on one HIP runtime; torch is used only
 for the multi-rank control plane (gloo: barrier, max-reduce, RCCL unique-id broadcast).
@@ -85,6 +87,48 @@ def kernel_bytes(s, ntr=1):
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
             "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "survey_pass": survey}
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+
+def _cpu_replica(job):
+    """One MPI-style replica: the oracle's full pass on strip p of P (spawned worker, no GPU)."""
+    config, full_depth, P, p, budget = job
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nx, ny, nl = synth.CONFIGS[config]
+    g = synth.make_mesh(nx, ny, nl, full_depth=full_depth)
+    m, _ = partition.local_mesh(g, partition.strip_parts(nx, ny, P), p)
+    del g
+    best, reps = O.time_full_pass(m, synth.make_fields(m), budget_s=budget)
+    return int((m.nlev_nod[: m.N].astype(np.int64) - 1).sum()), best, reps
+
+
+def cpu_all_cores(args, budget=4.0):
+    """P concurrent single-threaded oracle processes on a P-way partition of the workload mesh;
+    value = all owned cells / the slowest replica's best pass.  P = the cores this process may use,
+    at most 16 (the GPU box's CPU share per GPU)."""
+    import multiprocessing
+    P = max(1, min(16, len(os.sched_getaffinity(0))))
+    jobs = [(args.config, not args.parity_levels, P, p, budget) for p in range(P)]
+    with multiprocessing.get_context("spawn").Pool(P) as pool:
+        res = pool.map(_cpu_replica, jobs)
+    cells = sum(r[0] for r in res)
+    slowest = max(r[1] for r in res)
+    return {"value": round(cells / slowest, 1), "unit": "cell-updates/s", "cores": P,
+            "sample": f"{P} concurrent single-threaded oracle processes, y-strip partition of the same "
+                      f"{args.config} mesh (one-ring halo each), slowest replica's best of >= "
+                      f"{min(r[2] for r in res)} passes ({slowest:.3f} s/pass)"}
+
+
+def host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
 # ----------------------------------------------------------------------------- workload
@@ -188,6 +232,13 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+
+    # all-cores CPU baseline first: its worker processes are spawned before this process touches
+    # the GPU
+    cpu_all = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_all = cpu_all_cores(args)
+        log(f"cpu all cores: {cpu_all}")
 
     abi.dll()  # engine first: one HIP runtime for the process
     abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
@@ -347,7 +398,8 @@ def main():
         best, reps = O.time_full_pass(m, f, budget_s=args.cpu_budget)
         cpu = {"value": round(s["cn"] / best, 1), "unit": "cell-updates/s", "cores": 1, "kind": "port",
                "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
-                         f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)"}
+                         f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)",
+               "all_cores": cpu_all, "host": host_info()}
 
     check = None
     if args.check:
