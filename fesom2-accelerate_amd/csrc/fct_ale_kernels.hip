@@ -489,6 +489,8 @@ __device__ __forceinline__ void ldv_s(const real *__restrict__ p, real (&v)[C])
             v[c] = t.x;
             v[c + 1] = t.y;
         }
+    } else if constexpr (NT && C == 1) {
+        v[0] = __builtin_nontemporal_load(p);
     } else {
         ldv<C>(p, v);
     }
@@ -508,6 +510,8 @@ __device__ __forceinline__ void stv_s(real *__restrict__ p, const real (&v)[C], 
                 p[c] = v[c];
             }
         }
+    } else if constexpr (NT && C == 1) {
+        __builtin_nontemporal_store(v[0], p);
     } else {
         stv<C>(p, v, n);
     }
@@ -1731,7 +1735,7 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
 {
     const float invS = 1.0f / (float)S;
     const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real) + (size_t)G * sizeof(NodeRec);
-    const bool NT = (env_int("FESOM2_NT", 0) & 1) != 0;
+    const bool NT = (env_int("FESOM2_NT", 2) & 1) != 0;
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (NT) F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1793,18 +1797,23 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = a.nl - 1;
+    // levels per thread of the node kernel: FESOM2_P2_CPT (1 or 2; default as the other kernels)
+    const int C = (L % 2 == 0 && env_int("FESOM2_P2_CPT", levels_per_thread(L)) == 2) ? 2 : 1;
+    const int S = L / C, G = group_columns(S);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const int KB = env_int("FESOM2_P2_BATCH", 4);
     const size_t lds = (size_t)G * sizeof(NodeRec);
     if (C == 2) {
-        const bool NT = (env_int("FESOM2_NT", 0) & 2) != 0;
+        const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;  // measured: p2 streams non-temporal (-2 %)
         if (NT) F2A_LAUNCH_GROUPS((k_p2<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
+    if ((env_int("FESOM2_NT", 2) & 2) != 0) F2A_LAUNCH_GROUPS((k_p2<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
     if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
+    if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
@@ -1836,6 +1845,14 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
 #undef F2A_B3H_U
         if (NT) F2A_LAUNCH_GROUPS((k_b3h_u<2, 1, true>), tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
         F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+    }
+    {
+        // one level per thread (odd L): the same two-groups-per-block, non-temporal form
+        const int U = env_int("FESOM2_B3H_U", 2);
+        const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
+        const long ug = (groups + U - 1) / U * tr.n;
+        if (U == 2 && NT) F2A_LAUNCH_GROUPS((k_b3h_u<1, 2, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (U == 4 && NT) F2A_LAUNCH_GROUPS((k_b3h_u<1, 4, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
     }
     F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
 }

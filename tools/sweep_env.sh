@@ -1,11 +1,17 @@
 #!/bin/bash
-# usage: tools/sweep_env.sh "ENV=.. ENV=.." "ENV=.." ...   (one bench run per argument)
+# A/B sweep of environment knobs: tools/sweep_env.sh "ENV=.. ENV=.." "ENV=.." ...
+# Runs every configuration ROUNDS times, interleaved (A B C A B C ...), because the GPU's clocks
+# drift over minutes of back-to-back runs; one line per run in gpurun_out/sweep.txt.
+# BENCH_ARGS (eval'ed: may quote), STEPS, ROUNDS.
 set -o pipefail
 out=gpurun_out/sweep.txt
 : > $out
-for cfg in "$@"; do
-  env $cfg timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-30} $BENCH_ARGS > gpurun_out/sw.json 2>gpurun_out/sw_err.log || exit 1
-  python -c "
-import json;d=json.load(open('gpurun_out/sw.json'))
-k=d['kernels'];print('$cfg |', d['ms_per_step'], {n:v['avg_ms'] for n,v in k.items()})" >> $out
+for r in $(seq 1 ${ROUNDS:-1}); do
+  for cfg in "$@"; do
+    eval "env $cfg timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-30} $BENCH_ARGS" \
+        > gpurun_out/sw.json 2> gpurun_out/sw_err.log || exit 1
+    python -c "
+import json;d=json.loads(open('gpurun_out/sw.json').read().strip().splitlines()[-1])
+k=d['kernels'];print('r$r $cfg |', d['ms_per_step'], {n:v['avg_ms'] for n,v in k.items()})" >> $out
+  done
 done
