@@ -1,6 +1,8 @@
 // f2a_host.hpp -- host-side helpers shared by the C-ABI translation units.
 #pragma once
 #include "f2a_internal.hpp"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "../../include/fesom2-accelerate.h"
 
 #include <memory>
@@ -8,6 +10,15 @@
 #include <vector>
 
 namespace f2a {
+
+// roctx range over one ABI entry (rocprofv3 --marker-trace shows the phases; no-op otherwise)
+struct PhaseRange {
+    explicit PhaseRange(const char *name) { roctxRangePush(name); }
+    ~PhaseRange() { roctxRangePop(); }
+    PhaseRange(const PhaseRange &) = delete;
+    PhaseRange &operator=(const PhaseRange &) = delete;
+};
+
 
 // ---- error reporting (stderr + thread-local last error, like the reference's errorHandling,
 //      include/fesom2-accelerate.h:38-46)

@@ -138,6 +138,7 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
                            void **nod2D_edges, void **elem2D_edges, int *vlimit, real *flux_eps,
                            real *bignumber, real *dt)
 {
+    const PhaseRange range("fct_ale_pre_comm_acc_");
     *alg_state = 0;
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = *myDim_nod2D + *eDim_nod2D, T = *myDim_elem2D, E = *myDim_edge2D;
@@ -236,6 +237,7 @@ void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void
                                    int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges,
                                    int *vlimit, real *flux_eps, real *bignumber, real *dt)
 {
+    const PhaseRange range("fct_ale_pre_comm_batched_acc_");
     *alg_state = 0;
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = *myDim_nod2D + *eDim_nod2D, T = *myDim_elem2D, E = *myDim_edge2D;
@@ -284,6 +286,7 @@ void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void
 void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,
                              void **fct_adf_v, int *myDim_nod2D, int *nl, void **nlevels_nod2D)
 {
+    const PhaseRange range("fct_ale_inter_comm_acc_");
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NL = *nl, L = NL - 1;
     if (!check_levels(NL, "fct_ale_inter_comm_acc_")) return;
@@ -301,6 +304,7 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
                             void **fct_adf_h, int *myDim_edge2D, int *nl, void **nlevels_elem2D,
                             int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges)
 {
+    const PhaseRange range("fct_ale_post_comm_acc_");
     (void)nod_in_elem2D_dim;
     const hipStream_t st = stream_of(s);
     const int E = *myDim_edge2D, NL = *nl, L = NL - 1;
@@ -333,6 +337,7 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
                     int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                     void **nod2D_edges, void **elem2D_edges, real *dt)
 {
+    const PhaseRange range("fct_ale_c_acc_");
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
     if (!check_levels(NL, "fct_ale_c_acc_")) return;
@@ -371,6 +376,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                              void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges, real *dt,
                              void **comm, void **halo, int ntr, const char *who)
 {
+    const PhaseRange range(who);
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;
     if (!check_levels(NL, who)) return;
@@ -527,6 +533,7 @@ static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_pl
                                 void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges, real *dt,
                                 const char *who)
 {
+    const PhaseRange range(who);
     *alg_state = 0;
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1;

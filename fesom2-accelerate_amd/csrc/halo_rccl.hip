@@ -223,6 +223,7 @@ static bool check_buffers(HaloPlan *p, Buffer *bp, Buffer *bm, int ntr, size_t s
 namespace f2a {
 hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm, int ntr, size_t stride, hipStream_t s)
 {
+    const PhaseRange range("halo_exchange_async");
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
     if (!c || !p || !check_buffers(p, bp, bm, ntr, stride)) return nullptr;
@@ -246,6 +247,7 @@ extern "C" {
 void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void **fct_plus,
                            void **fct_minus)
 {
+    const PhaseRange range("fct_ale_exchange_acc_");
     *istat = 1;
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
@@ -257,6 +259,7 @@ void fct_ale_exchange_acc_(int *istat, void **s, void **comm, void **plan, void 
 void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
                                    int *nod_columns, void **fct_plus, void **fct_minus)
 {
+    const PhaseRange range("fct_ale_exchange_batched_acc_");
     *istat = 1;
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);
@@ -273,6 +276,7 @@ void fct_ale_exchange_batched_acc_(int *istat, void **s, void **comm, void **pla
 void fesom2_exchange_nod_acc_(int *istat, void **s, void **comm, void **plan, int *ntracers,
                              int *nod_columns, void **field_a, void **field_b)
 {
+    const PhaseRange range("fesom2_exchange_nod_acc_");
     *istat = 1;
     Comm *c = comm_of(comm);
     HaloPlan *p = plan_of(plan);

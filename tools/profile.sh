@@ -7,7 +7,7 @@ tag=${1:-r01}
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 rm -rf "$out" && mkdir -p "$out"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d "$out/stats" -o run -- \
     python3 bench.py --no-cpu-baseline > "$out/bench_under_rocprof.json" 2> "$out/stats.err"
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum \
     --output-format csv -d "$out/rd" -o rd -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 \
