@@ -482,11 +482,17 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             etaken[e] = 1;
             einfo.push_back(make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e));
         };
-        for (int v : order)
+        plan->owner_cum.assign(1, 0);
+        for (int v : order) {
             for (int k = ptr[v]; k < ptr[v + 1]; k++)
                 if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
+            plan->owner_cum.push_back((int)einfo.size());  // edges owned by positions < k+1
+        }
         for (int e = 0; e < n_edges; e++)
             if (!etaken[e]) push_edge(e);
+        // edges in owner order (chunked phase 2: an edge belongs to its first visited endpoint)
+        d.p_edge_owner = plan->mem.upload(einfo);
+        if (!d.p_edge_owner) return fail("device allocation for the edge order failed");
         // interior / boundary split for the exchange overlap (stable: processing order kept)
         auto interior_edge = [&](const int4 &ei) { return ei.x < n_owned && ei.y < n_owned; };
         std::stable_partition(einfo.begin(), einfo.end(), interior_edge);

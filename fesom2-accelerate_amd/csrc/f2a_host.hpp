@@ -93,6 +93,8 @@ struct Plan {
     DeviceArrays mem;
     bool has_ring = false;
     int lmax_edges = 0;
+    std::vector<int> owner_cum;  // [n_owned + 1]: edges owned by processing positions < k
+
     // per-edge arrival counters of the fused b3h, grown to the largest tracer batch seen
     mutable DeviceArrays cnt_mem;
     mutable int *edge_cnt = nullptr;

@@ -86,6 +86,7 @@ struct MeshPlanDev {
     const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order,
                                           // interior edges (both endpoints owned) first
     int n_edge_interior = 0;
+    const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
     // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
@@ -146,6 +147,9 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
+// the same over an explicit edge list
+hipError_t launch_b3h_edges(const int4 *einfo, int count, int nl, const real *plus, const real *minus,
+                            real *adf_h, const Tracers &tr, hipStream_t s);
 // iter_yn phase 2 (docs/refactoring.md:227-229, :258-260, :265-290): node kernel = b3v writing
 // fct_adf_v2, LO update from the limited vertical and horizontal fluxes (recomputed in-thread from
 // plus/minus of both edge endpoints), then fct_adf_v <- fct_adf_v2 over the whole column; the

@@ -1820,13 +1820,18 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
+    return launch_b3h_edges(mp.p_edge_info + begin, count, nl, plus, minus, adf_h, tr, s);
+}
+
+hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus, const real *minus,
+                            real *adf_h, const Tracers &tr, hipStream_t s)
+{
     const int L = nl - 1;
     int C = levels_per_thread(L);
     if (C == 2 && L % 4 == 0 && env_int("FESOM2_B3H_CPT", 2) == 4) C = 4;  // 4 levels: 2 x 16 B per array
     const int S = L / C, G = group_columns(S);
     const long groups = (count + G - 1) / G;
     const float invS = 1.0f / (float)S;
-    const int4 *ei = mp.p_edge_info + begin;
     const long tg = groups * tr.n;
     if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
     if (C == 2) {

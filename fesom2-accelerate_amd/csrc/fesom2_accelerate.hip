@@ -431,6 +431,26 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
             !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
             return;
         if (!run("fct_ale_p2_b3h", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
+    } else if (const int chunk = getenv("FESOM2_P2_CHUNK") ? atoi(getenv("FESOM2_P2_CHUNK")) : 0;
+               chunk > 0 && !comm && d.p_edge_owner && (int)plan->owner_cum.size() == N + 1) {
+        // FESOM2_P2_CHUNK=n: phase 2 in chunks of n nodes of the processing order -- b3h on the edges
+        // the chunk owns, then the node kernel on its nodes, so the limited fct_adf_h and plus/minus
+        // are re-read from the Infinity Cache (every node's edges belong to its own or an earlier
+        // chunk).  Measured break-even at 60k-node chunks (p2 -15 %, b3h +11 % from 2 x 20
+        // launches); two-stream pipelining of the chunks was slower.
+        for (int c0 = 0; c0 < N; c0 += chunk) {
+            const int c1 = std::min(N, c0 + chunk);
+            const int e0 = plan->owner_cum[c0], e1 = plan->owner_cum[c1] + (c1 == N ? E - plan->owner_cum[N] : 0);
+            if (!run("fct_ale_b3_horizontal", st, [&] {
+                    return f2a::launch_b3h_edges(d.p_edge_owner + e0, e1 - e0, NL, dptr<real>(bplus), dptr<real>(bminus),
+                                                 dptr<real>(badfh), a.tr, st);
+                }))
+                return;
+            f2a::P2Args ac = a;
+            ac.nodes = d.node_rec + c0;
+            ac.count = c1 - c0;
+            if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, ac, st); })) return;
+        }
     } else {
         if (!run("fct_ale_b3_horizontal", st, [&] {
                 return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
