@@ -393,3 +393,15 @@ def test_sizes_beyond_int32():
     dll().fesom2_download_(h8.ref, arr(out), C.byref(st))
     assert st.value == 0 and np.array_equal(out, a)
     dll().fesom2_free_(h8.ref)
+
+
+@pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129, 200])
+@pytest.mark.parametrize("full", [False, True])
+def test_level_counts(nl, full):
+    """Level counts from the minimum to deep columns, odd and even L (one or two levels per thread,
+    columns per block from 1 to 64, 80-level columns and 128/199-level ones)."""
+    m = synth.make_mesh(40, 14, nl, full_depth=full)
+    f = synth.make_fields(m)
+    st, got = run_pass(m, f)
+    assert st == 9
+    check_pass(m, got, O.full_pass(m, f))
