@@ -419,6 +419,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     if (n_csr == n_owned && n_owned > 0 && m.nlev_nod) {
         const char *env = getenv("FESOM2_PATCH");
         const int patch = env ? atoi(env) : 64;
+        const char *senv = getenv("FESOM2_SUBPATCH");
+        const int sub = senv ? atoi(senv) : 0;
         std::vector<int> order;
         order.reserve(n_owned);
         if (patch <= 1) {
@@ -445,6 +447,33 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 }
                 for (size_t h = cur.size(); h < queue.size(); h++) seen[queue[h]] = 0;  // back to the pool
                 std::sort(cur.begin(), cur.end());
+                if (sub > 1 && (int)cur.size() > sub) {
+                    // FESOM2_SUBPATCH: cut the patch into compact BFS blobs of `sub` nodes (the
+                    // fused kernels' columns per block), so a block's columns share their clusters
+                    std::vector<int> blob, rest(cur);
+                    std::vector<char> in(cur.size(), 1);
+                    auto idx = [&](int v) { return (int)(std::lower_bound(cur.begin(), cur.end(), v) - cur.begin()); };
+                    size_t pos = 0;
+                    for (size_t taken = 0; taken < cur.size();) {
+                        while (!in[pos]) pos++;
+                        blob.assign(1, cur[pos]);
+                        in[pos] = 0;
+                        for (size_t h = 0; h < blob.size() && (int)blob.size() < sub; h++)
+                            for (int k = ptr[blob[h]]; k < ptr[blob[h] + 1] && (int)blob.size() < sub; k++) {
+                                const int w = other[k];
+                                if (w >= n_owned) continue;
+                                const int q = idx(w);
+                                if (q < (int)cur.size() && cur[q] == w && in[q]) {
+                                    in[q] = 0;
+                                    blob.push_back(w);
+                                }
+                            }
+                        std::sort(blob.begin(), blob.end());
+                        order.insert(order.end(), blob.begin(), blob.end());
+                        taken += blob.size();
+                    }
+                    continue;
+                }
                 order.insert(order.end(), cur.begin(), cur.end());
             }
         }
