@@ -88,6 +88,12 @@ int *plan_edge_counters(const Plan *p, int ntr)
     return p->edge_cnt;
 }
 
+int *plan_wf_state(const Plan *p)
+{
+    if (!p->wf_state) p->wf_state = static_cast<int *>(p->cnt_mem.alloc(sizeof(int) * (16 + (size_t)p->dev.wf_ntiles)));
+    return p->wf_state;
+}
+
 Buffer *need(void **h, size_t bytes, const char *name)
 {
     Buffer *b = buf(h, name);
@@ -522,6 +528,68 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // edges in owner order (chunked phase 2: an edge belongs to its first visited endpoint)
         d.p_edge_owner = plan->mem.upload(einfo);
         if (!d.p_edge_owner) return fail("device allocation for the edge order failed");
+        // persistent phase-2 plan (MeshPlanDev::wf_*): tiles of the fused kernels' G positions
+        {
+            const int WG = f2a::fused_group_columns(nl);
+            const int ntiles = (n_owned + WG - 1) / WG;
+            std::vector<int> pos(n_owned);
+            for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
+            int sf[f2a::kWfStreams + 1];
+            for (int x = 0; x <= f2a::kWfStreams; x++) sf[x] = (int)((long)x * ntiles / f2a::kWfStreams);
+            auto stream_of_tile = [&](int t) {
+                int x = 0;
+                while (t >= sf[x + 1]) x++;
+                return x;
+            };
+            std::vector<int> owner(n_edges, -1), cnt(ntiles + 1, 0);
+            std::vector<int4> cross;
+            for (int e = 0; e < n_edges; e++) {
+                const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
+                const int t1 = n1 < n_owned ? pos[n1] / WG : -1, t2 = n2 < n_owned ? pos[n2] / WG : -1;
+                const int4 ei = make_int4(n1, n2, lev[e], e);
+                if (t1 >= 0 && t2 >= 0 && stream_of_tile(t1) != stream_of_tile(t2)) {
+                    cross.push_back(ei);
+                } else {
+                    owner[e] = t1 < 0 ? t2 : (t2 < 0 ? t1 : std::min(t1, t2));
+                    if (owner[e] >= 0) cnt[owner[e] + 1]++;
+                }
+            }
+            for (int t = 0; t < ntiles; t++) cnt[t + 1] += cnt[t];
+            std::vector<int4> wfe(cnt[ntiles]);
+            {
+                std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+                for (int e = 0; e < n_edges; e++)
+                    if (owner[e] >= 0)
+                        wfe[fill[owner[e]]++] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
+            }
+            std::vector<int> dptr(1, 0), deps;
+            for (int t = 0; t < ntiles; t++) {
+                const size_t d0 = deps.size();
+                for (int k = t * WG; k < std::min(n_owned, (t + 1) * WG); k++) {
+                    const int v = order[k];
+                    for (int q = ptr[v]; q < ptr[v + 1]; q++) {
+                        const int o = owner[refs[q].edge];
+                        if (o < 0 || o == t) continue;
+                        if (std::find(deps.begin() + d0, deps.end(), o) == deps.end()) deps.push_back(o);
+                    }
+                }
+                dptr.push_back((int)deps.size());
+            }
+            d.wf_G = WG;
+            d.wf_ntiles = ntiles;
+            d.wf_ncross = (int)cross.size();
+            for (int x = 0; x <= f2a::kWfStreams; x++) d.wf_stream_first[x] = sf[x];
+            d.wf_edges = plan->mem.upload(wfe);
+            d.wf_cross = plan->mem.upload(cross);
+            d.wf_edge_ptr = plan->mem.upload(cnt);
+            d.wf_dep_ptr = plan->mem.upload(dptr);
+            d.wf_deps = plan->mem.upload(deps);
+            if (!d.wf_edges || !d.wf_cross || !d.wf_edge_ptr || !d.wf_dep_ptr || !d.wf_deps)
+                return fail("device allocation for the persistent phase-2 plan failed");
+            if (getenv("FESOM2_PLAN_STATS"))
+                fprintf(stderr, "fesom2-accelerate: wavefront G=%d tiles=%d cross edges=%zu deps/tile %.2f\n", WG, ntiles,
+                        cross.size(), (double)deps.size() / std::max(ntiles, 1));
+        }
         // interior / boundary split for the exchange overlap (stable: processing order kept)
         auto interior_edge = [&](const int4 &ei) { return ei.x < n_owned && ei.y < n_owned; };
         std::stable_partition(einfo.begin(), einfo.end(), interior_edge);

@@ -87,6 +87,13 @@ struct MeshPlanDev {
                                           // interior edges (both endpoints owned) first
     int n_edge_interior = 0;
     const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
+    // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of
+    // consecutive tiles; per tile the owned edges in wf_edges[wf_edge_ptr[t] ..), the earlier tiles
+    // whose edges it needs in wf_deps[wf_dep_ptr[t] ..); edges between streams pre-limited (wf_cross)
+    int wf_G = 0, wf_ntiles = 0, wf_ncross = 0;
+    int wf_stream_first[9] = {};
+    const int4 *wf_edges = nullptr, *wf_cross = nullptr;
+    const int *wf_edge_ptr = nullptr, *wf_dep_ptr = nullptr, *wf_deps = nullptr;
     // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
@@ -143,6 +150,10 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
 // last at an edge's counter -- after its block has read the raw column -- writes the limited
 // fct_adf_h.
 constexpr int kMaxFusedDegree = 32;
+constexpr int kWfStreams = 8;  // one ticket stream per XCD
+// persistent phase 2 (b3h + node kernel interleaved per tile; single tracer, no exchange overlap).
+// `state` = zeroed ints: [0, 8) tickets, [8] timeout, [16, 16 + wf_ntiles) tile flags.
+hipError_t launch_p2_wavefront(const MeshPlanDev &mp, const P2Args &a, int *state, hipStream_t s);
 hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,

@@ -573,7 +573,15 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
 
 // Gather the fct_adf_h levels z0..z0+C-1 of a node's edges (CSR slice [e0, e1), ascending edge
 // order) and hand each (value, second-endpoint flag) to `f(c, h, second)` in that order.
-template <int C, int kBatch, class F>
+// agent-coherent loads (read-only data another workgroup of this launch published: no L1 hit)
+template <int C>
+__device__ __forceinline__ void ldv_coh(const real *p, real (&v)[C])
+{
+#pragma unroll
+    for (int c = 0; c < C; c++) v[c] = __hip_atomic_load(p + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int C, int kBatch, bool COH = false, class F>
 __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
                                           const real *__restrict__ adf_h, int z0, int L, F &&f)
 {
@@ -590,7 +598,10 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             if (z0 < (code[k] >> 1)) {
-                ldv<C>(adf_h + idx[k], h[k]);
+                if constexpr (COH)
+                    ldv_coh<C>(adf_h + idx[k], h[k]);
+                else
+                    ldv<C>(adf_h + idx[k], h[k]);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;
@@ -823,26 +834,14 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
 // interface below a thread's levels is recomputed in-thread from plus/minus (the bottom interface
 // nlev-1 is never limited); the barrier orders every raw fct_adf_v read of the block before its
 // writes.
-template <int C, int KB, bool NT>
-__global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
+// The node work of phase 2 for the block's G columns (records staged): see k_p2.  COH: fct_adf_h
+// read with agent-coherent loads (the persistent phase 2 publishes it inside the launch).
+template <int C, int KB, bool NT, bool COH>
+__device__ __forceinline__ void p2_node_work(const MeshPlanDev &mp, P2Args &a, const NodeRec *recs, int ncol,
+                                             float invS)
 {
-    extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = L / C;
     const int t = threadIdx.x;
-    int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
-    if (tr) {
-        a.plus += tr * a.tr.node;
-        a.minus += tr * a.tr.node;
-        a.ttf += tr * a.tr.node;
-        a.LO += tr * a.tr.node;
-        a.del_v += tr * a.tr.node;
-        a.del_h += tr * a.tr.node;
-        a.adf_v += tr * a.tr.lev;
-        a.adf_h += tr * a.tr.edge;
-    }
-    const int ncol = min(G, a.count - first);
-    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
     int j, u;
     slot_of(t, S, invS, j, u);
     const int z0 = C * u;
@@ -906,8 +905,8 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
             auto add = [&](int c, real h, int second) {
                 dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
             };
-            for_edges<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
-            if (ne > kRecEdge) for_edges<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+            for_edges<C, KB, COH>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+            if (ne > kRecEdge) for_edges<C, KB, COH>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
         }
     }
     __syncthreads();
@@ -918,6 +917,27 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     if (nw <= 0) return;
     stv_s<C, NT>(a.del_v + b, dv, nw);
     stv_s<C, NT>(a.del_h + b, dh, nw);
+}
+
+template <int C, int KB, bool NT>
+__global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G]
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.del_v += tr * a.tr.node;
+        a.del_h += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+    }
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+    p2_node_work<C, KB, NT, false>(mp, a, recs, ncol, invS);
 }
 
 // Phase-1 edge loop that also gathers the cluster (MeshPlanDev::edge_cluster): per edge the raw
@@ -1409,6 +1429,105 @@ __global__ __launch_bounds__(1024) void k_p2f(MeshPlanDev mp, P2Args a, int G, f
     }
 }
 
+// ---------------------------------------------------------------- persistent phase 2
+// b3-horizontal of `count` edges of `ei` by the whole block ((edge, slot) items strided over the
+// threads).  The raw flux is read and the limited one written agent-coherently: the node parts of
+// other workgroups of this launch read it (write-through stores, no L1 copy; MI355X guide §6 G16).
+template <int C>
+__device__ __forceinline__ void b3h_block_coherent(const int4 *__restrict__ ei, int count, int L, int S,
+                                                   float invS, const real *__restrict__ plus,
+                                                   const real *__restrict__ minus, real *adf_h)
+{
+    constexpr int K = 2;  // items per round: every load of K items issued before any is used
+    const int n = count * S;
+    for (int base = threadIdx.x; base < n; base += K * (int)blockDim.x) {
+        int4 e[K];
+        int z0[K];
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const int it = base + q * (int)blockDim.x;
+            int k = 0, u = 0;
+            if (it < n) slot_of(it, S, invS, k, u);
+            e[q] = it < n ? ei[k] : make_int4(0, 0, 0, 0);
+            z0[q] = C * u;
+        }
+        real f[K][C], p1[K][C], m1[K][C], p2[K][C], m2[K][C];
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            if (z0[q] >= e[q].z) continue;
+            ldv_coh<C>(adf_h + (size_t)e[q].w * L + z0[q], f[q]);
+            ldv<C>(plus + (size_t)e[q].x * L + z0[q], p1[q]);
+            ldv<C>(minus + (size_t)e[q].x * L + z0[q], m1[q]);
+            ldv<C>(plus + (size_t)e[q].y * L + z0[q], p2[q]);
+            ldv<C>(minus + (size_t)e[q].y * L + z0[q], m2[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const int nw = min(C, e[q].z - z0[q]);
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                if (c < nw)
+                    __hip_atomic_store(adf_h + (size_t)e[q].w * L + z0[q] + c,
+                                       b3h_factor(f[q][c], p1[q][c], m1[q][c], p2[q][c], m2[q][c]) * f[q][c],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Phase 2 as one persistent launch: workgroup w takes tiles (G positions of the processing order)
+// from ticket stream w % 8 in order; per tile it limits the edges the tile owns (its first visited
+// endpoint is in the tile), publishes the tile's flag, waits for the flags of the earlier tiles that
+// own its other edges, and runs the node kernel on the tile -- the limited fct_adf_h and plus/minus
+// it reads were touched moments before, in the caches.  Edge parts never wait and a tile only waits
+// for earlier tiles of its own stream, which are already claimed, so every wait ends (spins are
+// bounded regardless: state[8] records a timeout).  Edges between streams were limited before the
+// launch.
+template <int C, int KB>
+__global__ __launch_bounds__(1024) void k_p2w(MeshPlanDev mp, P2Args a, int *state, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G] | ticket
+    int *sh = reinterpret_cast<int *>(reinterpret_cast<NodeRec *>(lds) + G);
+    const int L = a.nl - 1, S = L / C;
+    const int x = blockIdx.x % kWfStreams;
+    const int tend = mp.wf_stream_first[x + 1];
+    int *flags = state + 16;
+    for (;;) {
+        if (threadIdx.x == 0) sh[0] = mp.wf_stream_first[x] + atomicAdd(state + x, 1);
+        __syncthreads();
+        const int tile = sh[0];
+        if (tile >= tend) return;
+        const int e0 = mp.wf_edge_ptr[tile];
+        b3h_block_coherent<C>(mp.wf_edges + e0, mp.wf_edge_ptr[tile + 1] - e0, L, S, invS, a.plus, a.minus, a.adf_h);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(flags + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x < 64) {  // one wave polls the tile's dependencies, relaxed, with back-off
+            for (int d = mp.wf_dep_ptr[tile] + (int)threadIdx.x; d < mp.wf_dep_ptr[tile + 1]; d += 64) {
+                const int dep = mp.wf_deps[d];
+                for (unsigned spins = 0;
+                     __hip_atomic_load(flags + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; spins++) {
+                    __builtin_amdgcn_s_sleep(2);
+                    // bounded: after ~1 s of spinning, or once any wait timed out, give up (the
+                    // launch's results are then invalid and state[8] says so)
+                    if (spins > (1u << 22) ||
+                        ((spins & 1023) == 1023 &&
+                         __hip_atomic_load(state + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                        __hip_atomic_store(state + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int first = tile * G;
+        const int ncol = min(G, a.count - first);
+        const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+        P2Args b = a;
+        p2_node_work<C, KB, true, true>(mp, b, recs, ncol, invS);
+        __syncthreads();  // LDS and the ticket slot are reused by the next tile
+    }
+}
+
 // iter_yn phase 2, nodes (see P2IterArgs).  Every slot of a column also copies fct_adf_v2 into
 // fct_adf_v for the levels the iteration does not assign (nz = 1, the bottom interface and the dry
 // levels: the Fortran's whole-array `fct_adf_v = fct_adf_v2`); the last slot covers level nl-1.
@@ -1875,6 +1994,35 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
         F2A_LAUNCH_GROUPS((k_p2f<2, 2>), groups, G, S, lds, s, mp, a, G, invS);
     }
     F2A_LAUNCH_GROUPS((k_p2f<1, 2>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_p2_wavefront(const MeshPlanDev &mp, const P2Args &a, int *state, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    if (G != mp.wf_G || a.tr.n != 1 || a.nodes != mp.node_rec || a.count != mp.n_owned) return hipErrorInvalidValue;
+    if (mp.wf_ncross > 0) {
+        const hipError_t e = launch_b3h_edges(mp.wf_cross, mp.wf_ncross, a.nl, a.plus, a.minus, a.adf_h, a.tr, s);
+        if (e != hipSuccess) return e;
+    }
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec) + 16;
+    const unsigned threads = threads_for(G, S);
+    int dev = 0, ncu = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (C == 2)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_p2w<2, 4>, threads, lds);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_p2w<1, 4>, threads, lds);
+    long grid = (long)std::max(1, per_cu) * std::max(ncu, 1);
+    if (getenv("FESOM2_PLAN_STATS")) fprintf(stderr, "fesom2-accelerate: wavefront grid %ld (%d per CU)\n", grid, per_cu);
+    grid = std::max<long>(kWfStreams, grid / kWfStreams * kWfStreams);
+    init_swizzle();
+    if (C == 2)
+        hipLaunchKernelGGL((k_p2w<2, 4>), dim3((unsigned)grid), dim3(threads), lds, s, mp, a, state, G, invS);
+    else
+        hipLaunchKernelGGL((k_p2w<1, 4>), dim3((unsigned)grid), dim3(threads), lds, s, mp, a, state, G, invS);
+    return hipGetLastError();
 }
 
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)

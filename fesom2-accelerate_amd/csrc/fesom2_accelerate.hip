@@ -431,6 +431,16 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
             !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
             return;
         if (!run("fct_ale_p2_b3h", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
+    } else if (const char *wf = getenv("FESOM2_P2_WF");
+               wf && atoi(wf) && !comm && ntr == 1 && d.wf_ntiles > 0 && d.wf_G == f2a::fused_group_columns(NL)) {
+        // phase 2 as one persistent launch (b3h and the node kernel interleaved per tile)
+        int *state = plan_wf_state(plan);
+        if (!state || !ok(hipMemsetAsync(state, 0, sizeof(int) * (16 + (size_t)d.wf_ntiles), st), "hipMemsetAsync(wf)"))
+            return;
+        f2a::P2Args aw = a;
+        aw.nodes = d.node_rec;
+        aw.count = N;
+        if (!run("fct_ale_p2_wavefront", st, [&] { return f2a::launch_p2_wavefront(d, aw, state, st); })) return;
     } else if (const int chunk = getenv("FESOM2_P2_CHUNK") ? atoi(getenv("FESOM2_P2_CHUNK")) : 0;
                chunk > 0 && !comm && d.p_edge_owner && (int)plan->owner_cum.size() == N + 1) {
         // FESOM2_P2_CHUNK=n: phase 2 in chunks of n nodes of the processing order -- b3h on the edges
