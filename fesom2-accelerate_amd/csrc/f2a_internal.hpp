@@ -158,6 +158,8 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
+// chunk c's node kernel and the next chunk's b3h in one launch (node blocks first; one tracer)
+hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int4 *einfo, int n_edges, hipStream_t s);
 // the same over an explicit edge list
 hipError_t launch_b3h_edges(const int4 *einfo, int count, int nl, const real *plus, const real *minus,
                             real *adf_h, const Tracers &tr, hipStream_t s);

@@ -786,20 +786,17 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 // data load, so a thread keeps U x 5 loads in flight instead of 5 (memory-level parallelism), and
 // the grid has U times fewer blocks.  NT: fct_adf_h streamed with non-temporal loads/stores so the
 // gathered plus/minus columns keep the L2.
+// U edge groups starting at group `ug` (relative to einfo) of one tracer.
 template <int C, int U, bool NT>
-__global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, int n_edges, int L,
-                                                int G, float invS, const real *__restrict__ plus,
-                                                const real *__restrict__ minus,
-                                                real *__restrict__ adf_h, Tracers trs)
+__device__ __forceinline__ void b3h_groups(const int4 *__restrict__ einfo, int n_edges, int L, int G, float invS,
+                                           const real *__restrict__ plus, const real *__restrict__ minus,
+                                           real *__restrict__ adf_h, int ug)
 {
-    int j, u, tr;
+    int j, u;
     slot_of(threadIdx.x, L / C, invS, j, u);
     if (j >= G) return;
     const int z0 = C * u;
-    const int k0 = group_tracer(trs.n, tr, c_tracer_major & 2) * U * G + j;
-    plus += tr * trs.node;
-    minus += tr * trs.node;
-    adf_h += tr * trs.edge;
+    const int k0 = ug * U * G + j;
     int4 ei[U];
 #pragma unroll
     for (int q = 0; q < U; q++) {
@@ -827,6 +824,18 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
         for (int c = 0; c < C; c++) out[c] = b3h_factor(f[q][c], p1[q][c], m1[q][c], p2[q][c], m2[q][c]) * f[q][c];
         stv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, out, nw);
     }
+}
+
+template <int C, int U, bool NT>
+__global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, int n_edges, int L,
+                                                int G, float invS, const real *__restrict__ plus,
+                                                const real *__restrict__ minus,
+                                                real *__restrict__ adf_h, Tracers trs)
+{
+    int tr;
+    const int ug = group_tracer(trs.n, tr, c_tracer_major & 2);
+    b3h_groups<C, U, NT>(einfo, n_edges, L, G, invS, plus + tr * trs.node, minus + tr * trs.node,
+                         adf_h + tr * trs.edge, ug);
 }
 
 // Phase 2, nodes: b3v + cv + ch, G node columns per block.  fct_adf_h already holds the b3-limited
@@ -1429,6 +1438,29 @@ __global__ __launch_bounds__(1024) void k_p2f(MeshPlanDev mp, P2Args a, int G, f
     }
 }
 
+// Chunked phase 2 with the boundary between chunks merged (FESOM2_P2_CHUNK with
+// FESOM2_P2_MERGE=1): blocks [0, nb_p2) run the node kernel on chunk c (nb_p2 a multiple of 8, so
+// the XCD swizzle applies within each role), the rest b3h on the edges chunk c+1 owns.  The node
+// blocks come first in dispatch order; the edge blocks fill the CUs as they drain.
+template <int C, int KB, int U>
+__global__ __launch_bounds__(1024) void k_p2_b3h_chunk(MeshPlanDev mp, P2Args a, int nb_p2, int G, float invS,
+                                                       const int4 *__restrict__ einfo, int n_edges, int Gb,
+                                                       float invSb)
+{
+    extern __shared__ real lds[];  // NodeRec[G] (node blocks)
+    const int b = blockIdx.x;
+    if (b < nb_p2) {
+        const int first = xcd_tile(b, nb_p2) * G;
+        if (first >= a.count) return;
+        const int ncol = min(G, a.count - first);
+        const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+        p2_node_work<C, KB, true, false>(mp, a, recs, ncol, invS);
+    } else {
+        const int nb = gridDim.x - nb_p2;
+        b3h_groups<C, U, true>(einfo, n_edges, a.nl - 1, Gb, invSb, a.plus, a.minus, a.adf_h, xcd_tile(b - nb_p2, nb));
+    }
+}
+
 // ---------------------------------------------------------------- persistent phase 2
 // b3-horizontal of `count` edges of `ei` by the whole block ((edge, slot) items strided over the
 // threads).  The raw flux is read and the limited one written agent-coherently: the node parts of
@@ -1994,6 +2026,22 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
         F2A_LAUNCH_GROUPS((k_p2f<2, 2>), groups, G, S, lds, s, mp, a, G, invS);
     }
     F2A_LAUNCH_GROUPS((k_p2f<1, 2>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int4 *einfo, int n_edges, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    if (C != 2 || a.tr.n != 1 || G * S != (int)threads_for(G, S)) return hipErrorInvalidValue;
+    const int U = 2;
+    const int nb_p2 = ((a.count + G - 1) / G + 7) / 8 * 8;
+    const int nb_b3h = (n_edges + U * G - 1) / (U * G);
+    const size_t lds = (size_t)G * sizeof(NodeRec);
+    const float invS = 1.0f / (float)S;
+    init_swizzle();
+    if (nb_p2 + nb_b3h > 0)
+        hipLaunchKernelGGL((k_p2_b3h_chunk<2, 4, 2>), dim3((unsigned)(nb_p2 + nb_b3h)), dim3(threads_for(G, S)), lds, s, mp,
+                           a, nb_p2, G, invS, einfo, n_edges, G, invS);
+    return hipGetLastError();
 }
 
 hipError_t launch_p2_wavefront(const MeshPlanDev &mp, const P2Args &a, int *state, hipStream_t s)

@@ -448,6 +448,35 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         // are re-read from the Infinity Cache (every node's edges belong to its own or an earlier
         // chunk).  Measured break-even at 60k-node chunks (p2 -15 %, b3h +11 % from 2 x 20
         // launches); two-stream pipelining of the chunks was slower.
+        const bool merge = getenv("FESOM2_P2_MERGE") && atoi(getenv("FESOM2_P2_MERGE")) && ntr == 1 &&
+                           (NL - 1) % 2 == 0;
+        auto edge_range = [&](int c0) {
+            const int c1 = std::min(N, c0 + chunk);
+            return std::make_pair(plan->owner_cum[c0], plan->owner_cum[c1] + (c1 == N ? E - plan->owner_cum[N] : 0));
+        };
+        if (merge) {
+            // b3h(0); then node kernel (c) + b3h(c+1) per launch; the last node kernel alone
+            const auto r0 = edge_range(0);
+            if (!run("fct_ale_b3_horizontal", st, [&] {
+                    return f2a::launch_b3h_edges(d.p_edge_owner + r0.first, r0.second - r0.first, NL, dptr<real>(bplus),
+                                                 dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
+                }))
+                return;
+            for (int c0 = 0; c0 < N; c0 += chunk) {
+                f2a::P2Args ac = a;
+                ac.nodes = d.node_rec + c0;
+                ac.count = std::min(N, c0 + chunk) - c0;
+                if (c0 + chunk < N) {
+                    const auto r = edge_range(c0 + chunk);
+                    if (!run("fct_ale_p2_b3h_chunk", st, [&] {
+                            return f2a::launch_p2_b3h_chunk(d, ac, d.p_edge_owner + r.first, r.second - r.first, st);
+                        }))
+                        return;
+                } else if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, ac, st); })) {
+                    return;
+                }
+            }
+        } else
         for (int c0 = 0; c0 < N; c0 += chunk) {
             const int c1 = std::min(N, c0 + chunk);
             const int e0 = plan->owner_cum[c0], e1 = plan->owner_cum[c1] + (c1 == N ? E - plan->owner_cum[N] : 0);

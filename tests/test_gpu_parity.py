@@ -91,7 +91,8 @@ KNOBS = [{"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "0"}, {"FESOM2_B3H_U": "4", "FES
          {"FESOM2_P1_STAGE": "1", "FESOM2_P1_EDGE": "0", "FESOM2_P1S_EB": "4"}, {"FESOM2_P1_EDGE": "0"},
          {"FESOM2_P1E_EB": "1"}, {"FESOM2_P1E_EB": "4"}, {"FESOM2_NT": "0"}, {"FESOM2_P2_CPT": "1"},
          {"FESOM2_P2_CPT": "1", "FESOM2_NT": "0"}, {"FESOM2_P2_CHUNK": "1000"},
-         {"FESOM2_P2_CHUNK": "37", "FESOM2_B3H_NT": "0"}, {"FESOM2_P2_WF": "1"}]
+         {"FESOM2_P2_CHUNK": "37", "FESOM2_B3H_NT": "0"}, {"FESOM2_P2_WF": "1"},
+         {"FESOM2_P2_CHUNK": "1000", "FESOM2_P2_MERGE": "1"}, {"FESOM2_P2_CHUNK": "333", "FESOM2_P2_MERGE": "1"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
