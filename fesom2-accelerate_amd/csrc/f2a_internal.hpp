@@ -132,6 +132,8 @@ struct P1Args {
     Tracers tr;
 };
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
+// opt-in phase-1 variants (fct_ale_variants.hip): *handled = false when no switch selects one
+hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool *handled);
 
 struct P2Args {
     int nl;

@@ -7,7 +7,8 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 
 
 def lib_path(name):
-    path = os.path.join(LIB_DIR, name)
+    # FESOM2_LIB_DIR: another build of the libraries (A/B measurements of two versions)
+    path = os.path.join(os.environ.get("FESOM2_LIB_DIR", LIB_DIR), name)
     if not os.path.exists(path):
         raise RuntimeError(
             f"{name} is not built ({path}); run `make -C fesom2-accelerate_amd` or __graft_entry__.build()")
