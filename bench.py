@@ -4,10 +4,13 @@
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
 ``torch.distributed.run`` with one rank per GPU.  Rank 0 prints ONE JSON line.
 
-* step      one full pass of the hot path over one batch (one tracer) of synthetic input:
-            fct_ale_pre_comm_acc_ (a1..b2, fused) -> fct_ale_post_comm_c_acc_ (b3h, b3v, cv, ch);
-            N > 1: fct_ale_exchange_post_comm_c_acc_ (RCCL halo of fct_plus/fct_minus on a second
-            stream, overlapped with the interior part of phase 2).
+* step      one full pass of the hot path over one batch (one tracer) of synthetic input, split by
+            direction (default --path split): fct_ale_pre_comm_v_acc_ (a1..b2 + b3v + cv: the
+            vertical half of phase 2 needs only the node's own column) -> fct_ale_post_comm_h_acc_
+            (b3h + ch; N > 1: the RCCL halo of fct_plus/fct_minus on a second stream, overlapped
+            with the interior edges/nodes).  --path fused: fct_ale_pre_comm_acc_ ->
+            fct_ale_post_comm_c_acc_ (or its exchange-overlapped form); --path stepwise: one kernel
+            per reference step.
             Device resident: inputs are in HBM before the timed region, no host copies inside it.
 * workload  BASELINE.json configs[2]: 1.2M-node x 80-level synthetic mesh (1600 x 750 periodic
             structured triangulation, full depth), 1 tracer, fp64 -- per GPU.  N > 1 is weak scaling:
@@ -84,9 +87,14 @@ def kernel_bytes(s, ntr=1):
     # p2 with b3h folded in: p2 + the limited adf_h written once (the other endpoint's plus/minus
     # columns are re-reads of arrays p2 already reads)
     p2f = p2 + ntr * 8 * ce
+    # split by direction: phase 1 + b3v/cv (adds the limited adf_v write, del_v rw; hnode, hnode_new,
+    # area shared), then c-horizontal alone (del_h rw, adf_h; area shared)
+    p1v = p1 + ntr * 8 * (cn + 2 * cn) + 8 * 3 * cn
+    p2h = ntr * 8 * (2 * cn + ce) + 8 * cn + 4 * N + ints_edges
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
-            "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "survey_pass": survey}
+            "fct_ale_p1v": p1v, "fct_ale_p2h": p2h,
+            "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -211,7 +219,9 @@ def main():
     ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
-    ap.add_argument("--path", default="fused", choices=["fused", "stepwise"])
+    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise"],
+                    help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
+                         "stepwise: one kernel per reference step")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
     ap.add_argument("--check", action="store_true",
@@ -260,12 +270,12 @@ def main():
 
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
-    if args.tracers > 1 and args.path != "fused":
-        raise SystemExit("--tracers > 1 runs the batched (fused) entry points only")
+    if args.tracers > 1 and args.path == "stepwise":
+        raise SystemExit("--tracers > 1 runs the batched (fused or split) entry points only")
     fields = synth.make_tracer_fields(m, args.tracers)
     f = fields[0]
     abi.set_resident(True)
-    abi.set_path(args.path)
+    abi.set_path("stepwise" if args.path == "stepwise" else "fused")
     dm = engine.DeviceMesh(m)
     dm.prepare()
     e = engine.FctAle(dm, f, copy=False) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
@@ -301,6 +311,18 @@ def main():
         e.upload("minus", pm[1].reshape(-1))
 
     def step():
+        if args.path == "split":
+            s1 = e.pre_comm_v()
+            if s1 != 7:
+                raise RuntimeError(f"pre_comm_v alg_state {s1}: {abi.last_error()}")
+            if world > 1 and args.exchange == "host":
+                host_exchange()
+                s2 = e.post_comm_h()
+            else:
+                s2 = e.post_comm_h(halo.comm, halo.plan) if halo is not None else e.post_comm_h()
+            if s2 != 9:
+                raise RuntimeError(f"post_comm_h alg_state {s2}: {abi.last_error()}")
+            return
         s1 = e.pre_comm()
         if s1 != 6:
             raise RuntimeError(f"pre_comm alg_state {s1}: {abi.last_error()}")

@@ -130,8 +130,14 @@ struct P1Args {
     real *plus, *minus;
     real dt, eps, big;
     Tracers tr;
+    // vertical part of phase 2 in the same kernel (launch_p1v: b3v + cv on the own column)
+    const real *area = nullptr, *hnode = nullptr, *hnode_new = nullptr;
+    real *del_v = nullptr;
 };
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
+// phase 1 + the vertical half of phase 2 (b3v, cv need only the node's own column: no halo), then
+// phase 2's horizontal half alone (launch_p2h: c-horizontal; b3h stays its own kernel)
+hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // opt-in phase-1 variants (fct_ale_variants.hip): *handled = false when no switch selects one
 hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool *handled);
 
@@ -147,6 +153,7 @@ struct P2Args {
     int *edge_cnt = nullptr;  // fused b3h: zeroed per-edge(-per-tracer) arrival counters
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
+hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal folded into the node kernel (a.edge_cnt zeroed, mp.max_degree <= kMaxFusedDegree):
 // every endpoint limits its edges' fluxes itself for c-horizontal, and the endpoint that arrives
 // last at an edge's counter -- after its block has read the raw column -- writes the limited

@@ -310,7 +310,13 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // Phase 1: a1 + a2 + a3 + b1v + b1h + b2 for the block's G columns.  Before the barrier every
 // thread issues all of its loads (cluster gathers for tvert, edge gathers for b1h, its own column);
 // after it the vertical 3-point stencil of tvert is read from LDS and the limiter ratios stored.
-template <int VLIMIT, int C, int RB, int EB, bool NT>
+//
+// VERT: the vertical half of phase 2 follows in the same kernel (b3v + cv read only the node's own
+// column, so they need no halo exchange): plus/minus go through LDS to the neighbouring level slots,
+// fct_adf_v is limited from the raw values the thread already holds and written after the barriers
+// (every raw fct_adf_v read of the block happened before the first one), and del_ttf_advvert is
+// updated -- the arithmetic of k_p2, so results are identical.
+template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
@@ -325,6 +331,7 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         a.minus += tr * a.tr.node;
         a.adf_v += tr * a.tr.lev;
         a.adf_h += tr * a.tr.edge;
+        if (VERT) a.del_v += tr * a.tr.node;
     }
     const int ncol = min(G, a.n_owned - first);
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
@@ -340,10 +347,12 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
 #pragma unroll
     for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = 0.;
     size_t b = 0, ab = 0;
+    real v[C + 1];  // raw fct_adf_v at z0 .. z0+C (b1v; the VERT tail limits them)
+#pragma unroll
+    for (int c = 0; c <= C; c++) v[c] = 0.;
     if (nw > 0) {
         b = (size_t)ni.n * L + z0;
         ab = (size_t)ni.n * a.nl + z0;
-        real v[C + 1];
 #pragma unroll
         for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? ld1_s<NT>(a.adf_v + ab + c) : 0.;
 #pragma unroll
@@ -383,8 +392,11 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         }
     }
     __syncthreads();
-    if (nw == 0) return;
+    if (!VERT && nw == 0) return;
     real lo[C], ai[C], op[C], om[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) lo[c] = ai[c] = op[c] = om[c] = 0.;
+    if (nw > 0) {
     ldv<C>(a.LO + b, lo);
 #pragma unroll
     for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
@@ -428,6 +440,101 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     }
     stv_s<C, NT>(a.plus + b, op, nw);
     stv_s<C, NT>(a.minus + b, om, nw);
+    }
+    if constexpr (VERT) {
+        // ---- b3-vertical + c-vertical on the own column (as k_p2: docs/refactoring.md:204-233, :295-300)
+        __syncthreads();  // the tvert stencil reads are done: the LDS takes plus/minus
+        real *pl = lds, *mn = lds + G * L;
+        if (col) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                pl[q + c] = op[c];
+                mn[q + c] = om[c];
+            }
+        }
+        __syncthreads();
+        const int top = Ln > 1 ? Ln : 1;                   // the Fortran always limits nz = 1
+        const int na = col ? max(0, min(C, top - z0)) : 0;  // cells whose fct_adf_v is limited
+        if (na <= 0) return;
+        if (nw == 0) {  // no wet cell (nlevels_nod2D <= 1): only nz = 1 is limited, from memory
+            b = (size_t)ni.n * L + z0;
+            ab = (size_t)ni.n * a.nl + z0;
+#pragma unroll
+            for (int c = 0; c <= C; c++) v[c] = c < 2 ? a.adf_v[ab + c] : 0.;
+        }
+        real pp[C + 2], mm[C + 2];  // plus/minus at z0-1 .. z0+C
+        pp[0] = z0 ? pl[q - 1] : 0.;
+        mm[0] = z0 ? mn[q - 1] : 0.;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            pp[c + 1] = c < nw ? op[c] : (c < na ? a.plus[b + c] : 0.);
+            mm[c + 1] = c < nw ? om[c] : (c < na ? a.minus[b + c] : 0.);
+        }
+        const bool below = z0 + C < Ln;
+        pp[C + 1] = below ? pl[q + C] : 0.;
+        mm[C + 1] = below ? mn[q + C] : 0.;
+        real lim[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; c++) {
+            const int z = z0 + c;
+            const bool lim_here = (c < C) ? (z < top) : (z < Ln);
+            lim[c] = lim_here ? b3v_factor(z, v[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) * v[c] : v[c];
+        }
+        real dv[C];
+        if (nw > 0) {
+            real del_v[C], tt[C], hn[C], hnn[C];
+            ldv_s<C, NT>(a.del_v + b, del_v);
+            ldv<C>(a.ttf + b, tt);
+            ldv_s<C, NT>(a.hnode + b, hn);
+            ldv_s<C, NT>(a.hnode_new + b, hnn);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                const real dta = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+                real tv = del_v[c] - tt[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
+                tv = tv + lo[c] * hnn[c];
+                dv[c] = tv + (lim[c] - lim[c + 1]) * dta;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; c++)
+            if (c < na) st1_s<NT>(const_cast<real *>(a.adf_v) + ab + c, lim[c]);  // limited in place
+        if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
+    }
+}
+
+// Phase 2, horizontal half (after the exchange, with b3h): c-horizontal only (see k_p1 VERT).
+template <int C, int KB, bool NT>
+__global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G]
+    const int L = a.nl - 1, S = L / C;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.del_h += tr * a.tr.node;
+        a.adf_h += tr * a.tr.edge;
+    }
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+    int j, u;
+    slot_of(threadIdx.x, S, invS, j, u);
+    const int z0 = C * u;
+    if (j >= ncol) return;
+    const NodeInfo ni = recs[j].info;
+    const int nw = max(0, min(C, ni.Ln - z0));
+    if (nw <= 0) return;
+    const size_t b = (size_t)ni.n * L + z0, ab = (size_t)ni.n * a.nl + z0;
+    real dh[C], dta[C];
+    ldv_s<C, NT>(a.del_h + b, dh);
+#pragma unroll
+    for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+    const int ne = ni.e1 - ni.e0;
+    auto add = [&](int c, real h, int second) {
+        dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+    };
+    for_edges<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+    if (ne > kRecEdge) for_edges<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+    stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
 // Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
@@ -831,6 +938,38 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     case 88: return C == 2 ? p1_launch<2, 8, 8>(mp, a, s, G, S, groups) : p1_launch<1, 8, 8>(mp, a, s, G, S, groups);
     default: return C == 2 ? p1_launch<2, 2, 2>(mp, a, s, G, S, groups) : p1_launch<1, 2, 2>(mp, a, s, G, S, groups);
     }
+}
+
+hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+    if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
+    if (C == 2) {
+        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec);
+    const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;
+    if (C == 2) {
+        if (NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2h<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (NT) F2A_LAUNCH_GROUPS((k_p2h<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2h<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)

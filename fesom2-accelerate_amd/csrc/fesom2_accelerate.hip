@@ -228,23 +228,26 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
 // Batched phase 1 (a1..b2, fused) of ntracers tracers in one launch: per-tracer handles hold the
 // tracers one after another, (N+H)*L doubles apart (ttf, fct_LO, fct_plus, fct_minus), (N+H)*nl
 // apart (fct_adf_v) and E*L apart (fct_adf_h); area_inv is shared.  alg_state 6 on success.
-void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
-                                   void **fct_minus, void **ttf, void **fct_LO, void **fct_adf_v,
-                                   void **fct_adf_h, void **area_inv, int *myDim_nod2D,
-                                   int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
-                                   void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
-                                   void **nod_in_elem2D_num, void **nod_in_elem2D,
-                                   int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges,
-                                   int *vlimit, real *flux_eps, real *bignumber, real *dt)
+// Fused phase 1 of ntracers tracers; with `area` given (vertical = true) also b3v + cv on the own
+// columns (launch_p1v: fct_adf_v limited in place, del_ttf_advvert updated; alg_state 7).
+static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **fct_plus, void **fct_minus,
+                                void **ttf, void **fct_LO, void **fct_adf_v, void **fct_adf_h, void **area_inv,
+                                int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                                void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                                void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                                void **nod2D_edges, void **elem2D_edges, int *vlimit, real *flux_eps,
+                                real *bignumber, real *dt, void **area, void **hnode, void **hnode_new,
+                                void **del_ttf_advvert, const char *who)
 {
-    const PhaseRange range("fct_ale_pre_comm_batched_acc_");
+    const PhaseRange range(who);
+    const bool vertical = area != nullptr;
     *alg_state = 0;
     const hipStream_t st = stream_of(s);
     const int N = *myDim_nod2D, NT = *myDim_nod2D + *eDim_nod2D, T = *myDim_elem2D, E = *myDim_edge2D;
     const int NL = *nl, L = NL - 1, ntr = *ntracers;
-    if (!check_levels(NL, "fct_ale_pre_comm_batched_acc_")) return;
+    if (!check_levels(NL, who)) return;
     if (ntr < 1) {
-        report("fct_ale_pre_comm_batched_acc_: ntracers = %d", ntr);
+        report("%s: ntracers = %d", who, ntr);
         return;
     }
     MeshHandles mh;
@@ -265,6 +268,14 @@ void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void
     if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie || !mh.nie_num ||
         !bplus || !bminus || !bttf || !blo || !badfv || !badfh || !bainv)
         return;
+    Buffer *barea = nullptr, *bh = nullptr, *bhn = nullptr, *bdv = nullptr;
+    if (vertical) {
+        barea = need(area, col_bytes(N, NL), "area");
+        bh = need(hnode, col_bytes(N, L), "hnode");
+        bhn = need(hnode_new, col_bytes(N, L), "hnode_new");
+        bdv = need(del_ttf_advvert, ntr > 1 ? nodeb : col_bytes(N, L), "del_ttf_advvert");
+        if (!barea || !bh || !bhn || !bdv) return;
+    }
     mh.nlev_nod = bnlnod;
     const Plan *plan = get_plan(mh, N, NT, E, NL, true);
     if (!plan) return;
@@ -276,9 +287,63 @@ void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void
                   dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
                   *dt, *flux_eps, *bignumber};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    if (vertical) {
+        a.area = dptr<real>(barea);
+        a.hnode = dptr<real>(bh);
+        a.hnode_new = dptr<real>(bhn);
+        a.del_v = dptr<real>(bdv);
+        if (!run("fct_ale_p1v", st, [&] { return f2a::launch_p1v(plan->dev, a, st); })) return;
+        *alg_state = 7;
+        if (!g_resident)
+            for (Buffer *b : {bplus, bminus, badfv, bdv})
+                if (!d2h_async(b, st)) {
+                    *alg_state = 0;
+                    return;
+                }
+        return;
+    }
     if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) return;
     *alg_state = 6;
     if (!g_resident && (!d2h_async(bplus, st) || !d2h_async(bminus, st))) *alg_state = 0;
+}
+
+void fct_ale_pre_comm_batched_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus,
+                                   void **fct_minus, void **ttf, void **fct_LO, void **fct_adf_v,
+                                   void **fct_adf_h, void **area_inv, int *myDim_nod2D,
+                                   int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                                   void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                                   void **nod_in_elem2D_num, void **nod_in_elem2D,
+                                   int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges,
+                                   int *vlimit, real *flux_eps, real *bignumber, real *dt)
+{
+    pre_comm_fused_impl(alg_state, s, ntracers, fct_plus, fct_minus, ttf, fct_LO, fct_adf_v, fct_adf_h, area_inv,
+                        myDim_nod2D, eDim_nod2D, myDim_elem2D, myDim_edge2D, nl, nlevels_nod2D, nlevels_elem2D,
+                        elem2D_nodes, nod_in_elem2D_num, nod_in_elem2D, nod_in_elem2D_dim, nod2D_edges,
+                        elem2D_edges, vlimit, flux_eps, bignumber, dt, nullptr, nullptr, nullptr, nullptr,
+                        "fct_ale_pre_comm_batched_acc_");
+}
+
+// Phase 1 + the vertical half of phase 2 (b3v, cv: own columns only, no halo).  Then the exchange
+// and fct_ale_post_comm_h_acc_.  Same results as pre_comm + post_comm_c.
+void fct_ale_pre_comm_v_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus, void **fct_minus,
+                             void **ttf, void **fct_LO, void **fct_adf_v, void **fct_adf_h, void **area_inv,
+                             void **area, void **hnode, void **hnode_new, void **del_ttf_advvert,
+                             int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                             void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                             void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                             void **nod2D_edges, void **elem2D_edges, int *vlimit, real *flux_eps,
+                             real *bignumber, real *dt)
+{
+    if (!area) {
+        *alg_state = 0;
+        report("fct_ale_pre_comm_v_acc_: area handle missing");
+        return;
+    }
+    pre_comm_fused_impl(alg_state, s, ntracers, fct_plus, fct_minus, ttf, fct_LO, fct_adf_v, fct_adf_h, area_inv,
+                        myDim_nod2D, eDim_nod2D, myDim_elem2D, myDim_edge2D, nl, nlevels_nod2D, nlevels_elem2D,
+                        elem2D_nodes, nod_in_elem2D_num, nod_in_elem2D, nod_in_elem2D_dim, nod2D_edges,
+                        elem2D_edges, vlimit, flux_eps, bignumber, dt, area, hnode, hnode_new, del_ttf_advvert,
+                        "fct_ale_pre_comm_v_acc_");
 }
 
 // ----------------------------------------------------------------------------- phase 2
@@ -520,6 +585,71 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                 *alg_state = 0;
                 return;
             }
+}
+
+// Horizontal half of phase 2 after fct_ale_pre_comm_v_acc_: [RCCL halo exchange of fct_plus/minus
+// overlapped with the interior] + b3h + c-horizontal (comm / halo_plan may be null handles: the
+// halo is then already in place).  alg_state -> 9.
+void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **comm, void **halo_plan,
+                              void **fct_plus, void **fct_minus, void **fct_adf_h, void **del_ttf_advhoriz,
+                              void **area, int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                              void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges,
+                              void **elem2D_edges, real *dt)
+{
+    const PhaseRange range("fct_ale_post_comm_h_acc_");
+    *alg_state = 0;
+    const hipStream_t st = stream_of(s);
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, L = NL - 1, ntr = *ntracers;
+    if (!check_levels(NL, "fct_ale_post_comm_h_acc_")) return;
+    if (ntr < 1) {
+        report("fct_ale_post_comm_h_acc_: ntracers = %d", ntr);
+        return;
+    }
+    const bool exch = comm && *comm;
+    Buffer *bplus = need(fct_plus, col_bytes(NT, L) * ntr, "fct_plus");
+    Buffer *bminus = need(fct_minus, col_bytes(NT, L) * ntr, "fct_minus");
+    Buffer *badfh = need(fct_adf_h, col_bytes(E, L) * ntr, "fct_adf_h");
+    Buffer *bdh = need(del_ttf_advhoriz, ntr > 1 ? col_bytes(NT, L) * ntr : col_bytes(N, L), "del_ttf_advhoriz");
+    Buffer *barea = need(area, col_bytes(N, NL), "area");
+    Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    if (!bplus || !bminus || !badfh || !bdh || !barea || !bnl || !mh.edges || !mh.edge_tri || !mh.nlev_elem) return;
+    mh.nlev_nod = bnl;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    if (!plan) return;
+    const f2a::MeshPlanDev &d = plan->dev;
+    if (!g_resident && !exch && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
+    hipEvent_t halo_done = nullptr;
+    if (exch) {
+        halo_done = f2a::halo_exchange_async(comm, halo_plan, bplus, bminus, ntr, (size_t)NT * L, st);
+        if (!halo_done) return;
+    }
+    const int e_first = exch ? d.n_edge_interior : E, n_first = exch ? d.n_p2_interior : N;
+    f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), nullptr, nullptr, nullptr, nullptr,
+                  dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
+    a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    if (!run("fct_ale_b3_horizontal", st, [&] {
+            return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
+                                         a.tr, st);
+        }))
+        return;
+    if (!run("fct_ale_p2h", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
+    if (exch) {
+        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
+        if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
+                return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
+                                             dptr<real>(badfh), a.tr, st);
+            }))
+            return;
+        a.nodes = d.p2_rec + n_first;
+        a.count = N - n_first;
+        if (!run("fct_ale_p2h_boundary", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
+    }
+    *alg_state = 9;
+    if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
 }
 
 void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,

@@ -30,7 +30,7 @@ EXPORTS = (
     "fct_ale_pre_comm_batched_acc_", "fct_ale_post_comm_c_batched_acc_", "fct_ale_exchange_batched_acc_",
     "fct_ale_exchange_post_comm_c_batched_acc_", "fct_ale_post_comm_iter_acc_",
     "fct_ale_post_comm_iter_batched_acc_", "fesom2_exchange_nod_acc_",
-    "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_",
+    "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_", "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_",
 )
 
 _dll = None

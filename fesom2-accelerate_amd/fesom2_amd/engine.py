@@ -67,6 +67,8 @@ class FctAle:
     and bound as the handles' host pointers exactly like the Fortran arrays would be).
     """
 
+    ntr = 1  # tracers per call (FctAleBatch: several)
+
     def __init__(self, dmesh: DeviceMesh, fields, stream=None, vlimit=1, flux_eps=1e-16, bignumber=1e3,
                  dt=1.0, copy=True):
         m = dmesh.m
@@ -141,6 +143,36 @@ class FctAle:
             h["area"].ref, ip(m.N), ip(m.H), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
             d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
         return st.value
+
+    # ------------------------------------------------------------------ split by direction
+    def pre_comm_v(self):
+        """fct_ale_pre_comm_v_acc_: a1..b2 + b3v + cv (alg_state 7)."""
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        dll().fct_ale_pre_comm_v_acc_(
+            C.byref(st), self.stream.ref, ip(self.ntr), h["plus"].ref, h["minus"].ref, h["ttf"].ref, h["LO"].ref,
+            h["adf_v"].ref, h["adf_h"].ref, h["area_inv"].ref, h["area"].ref, h["hnode"].ref, h["hnode_new"].ref,
+            h["del_v"].ref, ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
+            d["elem2D_nodes"].ref, d["nie_num"].ref, d["nie"].ref, ip(m.dim), d["edges"].ref, d["edge_tri"].ref,
+            ip(self.vlimit), dp(self.eps), dp(self.big), dp(self.dt))
+        return st.value
+
+    def post_comm_h(self, comm=None, plan=None):
+        """fct_ale_post_comm_h_acc_: [exchange overlapped with the interior] + b3h + ch (alg_state 9)."""
+        m, h, d = self.m, self.h, self.dm.h
+        st = C.c_int(-1)
+        none = C.c_void_p()
+        dll().fct_ale_post_comm_h_acc_(
+            C.byref(st), self.stream.ref, ip(self.ntr), comm.ref if comm else C.byref(none),
+            plan.ref if plan else C.byref(none), h["plus"].ref, h["minus"].ref, h["adf_h"].ref, h["del_h"].ref,
+            h["area"].ref, ip(m.N), ip(m.H), ip(m.E), ip(m.nl), d["nlev_nod"].ref, d["nlev_elem"].ref,
+            d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
+        return st.value
+
+    def split_pass(self):
+        """Single-domain pass through the direction-split entries (final alg_state, 9 on success)."""
+        s1 = self.pre_comm_v()
+        return self.post_comm_h() if s1 == 7 else s1
 
     def _iter_buffers(self):
         """fct_adf_v2 / fct_adf_h2 (zero-initialised, as FESOM allocates them) on first use."""

@@ -228,6 +228,27 @@ void fct_ale_exchange_post_comm_c_batched_acc_(int *alg_state, void **s, void **
                                                int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                                                void **nod2D_edges, void **elem2D_edges, real_type *dt);
 
+/* ---- split by direction (the fastest pass): the vertical half of phase 2 (b3-vertical, c-vertical)
+ * reads only the node's own column, so it runs inside phase 1; phase 2 keeps b3-horizontal and
+ * c-horizontal.  Same results as pre_comm + post_comm_c.  ntracers as the batched entries (1 = the
+ * single-tracer layouts; fct_adf_v, del_ttf_advvert then sized like fct_ale_post_comm_c_acc_). */
+/* a1..b2 + b3v + cv: fct_plus/minus, limited fct_adf_v, del_ttf_advvert updated.  alg_state -> 7. */
+void fct_ale_pre_comm_v_acc_(int *alg_state, void **s, int *ntracers, void **fct_plus, void **fct_minus,
+                             void **ttf, void **fct_LO, void **fct_adf_v, void **fct_adf_h, void **area_inv,
+                             void **area, void **hnode, void **hnode_new, void **del_ttf_advvert,
+                             int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D, int *nl,
+                             void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                             void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                             void **nod2D_edges, void **elem2D_edges, int *vlimit, real_type *flux_eps,
+                             real_type *bignumber, real_type *dt);
+/* [halo exchange of fct_plus/minus overlapped with the interior, when *comm and *halo_plan are
+ * set] + b3h + c-horizontal.  alg_state -> 9. */
+void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **comm, void **halo_plan,
+                              void **fct_plus, void **fct_minus, void **fct_adf_h, void **del_ttf_advhoriz,
+                              void **area, int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                              void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges,
+                              void **elem2D_edges, real_type *dt);
+
 /* ---- iter_yn iterative FCT (docs/refactoring.md:227-229, :258-260, :265-290).
  * Phase 2 of a non-final iteration, after the exchange of fct_plus/minus: b3 limiting with the
  * remainders fct_adf_v2 = (1-ae) fct_adf_v (levels 2..nlevels-1) and fct_adf_h2 = (1-ae) fct_adf_h,

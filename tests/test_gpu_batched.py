@@ -170,3 +170,68 @@ def test_batched_partitioned_exchange(comm, overlap):
         for name, w in (("del_v", L), ("del_h", L), ("adf_v", nl)):
             got = partition.gather_owned(ms, lambda r: outs[r][name].reshape(ntr, -1)[k], w, g.N)
             assert np.array_equal(got, wants[k][name]), (name, k)
+
+
+def test_batched_split_by_direction():
+    m = synth.config_mesh("8k x 20")
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        for k in range(3):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+    finally:
+        e.free()
+        dm.free()
+
+
+def test_split_by_direction_partitioned_overlap(comm):
+    """Two partitions, 2 tracers, the split entries with the exchange inside fct_ale_post_comm_h_acc_
+    (deranged halo repaired only by the one-rank exchange, as test_batched_partitioned_exchange)."""
+    nx, ny, nl, ntr = 64, 48, 21, 2
+    g = synth.make_mesh(nx, ny, nl)
+    gtr = synth.make_tracer_fields(g, ntr)
+    wants = [O.full_pass(g, t) for t in gtr]
+    part = np.random.default_rng(9).integers(0, 2, g.N).astype(np.int32)
+    locs = [partition.local_mesh(g, part, r) for r in range(2)]
+    runs, plans, outs, pm = [], [], [], []
+    L = g.L
+    try:
+        for m, _ in locs:
+            dm = engine.DeviceMesh(m)
+            runs.append((dm, engine.FctAleBatch(dm, synth.make_tracer_fields(m, ntr))))
+        for _, e in runs:
+            assert e.pre_comm_v() == 7, abi.last_error()
+            e.sync()
+            pm.append([e.download("plus").reshape(ntr, -1, L), e.download("minus").reshape(ntr, -1, L)])
+        for r, (m, h) in enumerate(locs):
+            for q in h.neighbors:
+                src, dst = locs[q][1].send[r] - 1, h.recv[q] - 1
+                for a in range(2):
+                    pm[r][a][:, dst] = pm[q][a][:, src]
+            cols = np.arange(m.N, m.N + m.H)
+            nxt = np.roll(cols, -1)
+            for a, name in enumerate(("plus", "minus")):
+                stored = pm[r][a].copy()
+                stored[:, cols] = pm[r][a][:, nxt]
+                runs[r][1].upload(name, stored.reshape(-1))
+            plans.append(make_plan(cols + 1, nxt + 1, nl))
+        for (_, e), plan in zip(runs, plans):
+            assert e.post_comm_h(comm, plan) == 9, abi.last_error()
+        for _, e in runs:
+            e.sync()
+            outs.append({k: e.download(k) for k in ("del_v", "del_h", "adf_v")})
+    finally:
+        for plan in plans:
+            dll().fesom2_halo_plan_free_(plan.ref)
+        for dm, e in runs:
+            e.free()
+            dm.free()
+    ms = [m for m, _ in locs]
+    for k in range(ntr):
+        for name, w in (("del_v", L), ("del_h", L), ("adf_v", nl)):
+            got = partition.gather_owned(ms, lambda r: outs[r][name].reshape(ntr, -1)[k], w, g.N)
+            assert np.array_equal(got, wants[k][name]), (name, k)

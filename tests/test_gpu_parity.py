@@ -406,3 +406,42 @@ def test_level_counts(nl, full):
     st, got = run_pass(m, f)
     assert st == 9
     check_pass(m, got, O.full_pass(m, f))
+
+
+@pytest.mark.parametrize("name,full,perm", CASES + [("tiny", True, False)])
+@pytest.mark.parametrize("resident", [True, False])
+def test_split_by_direction_matches_oracle(name, full, perm, resident):
+    """fct_ale_pre_comm_v_acc_ (a1..b2 + b3v + cv) then fct_ale_post_comm_h_acc_ (b3h + ch): the
+    same results as the reference sequence, every output exact."""
+    m, f = mesh(name, full, perm)
+    want = O.full_pass(m, f)
+    abi.set_resident(resident)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        abi.set_resident(True)
+        e.free()
+        dm.free()
+    check_pass(m, got, want)
+
+
+@pytest.mark.parametrize("vlimit", [2, 3])
+def test_split_by_direction_vlimit(vlimit):
+    m, f = mesh("8k x 20")
+    st, p1 = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
+    want = O.post_comm(m, f, p1["plus"], p1["minus"])
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f, vlimit=vlimit)
+    try:
+        assert e.split_pass() == 9, abi.last_error()
+        e.sync()
+        for k in ("adf_v", "adf_h", "del_v", "del_h"):
+            assert np.array_equal(e.download(k), want[k]), k
+    finally:
+        e.free()
+        dm.free()
