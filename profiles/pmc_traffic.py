@@ -19,14 +19,23 @@ import csv
 import json
 import sys
 
-NAMES = {"k_p1": "fct_ale_p1", "k_p2": "fct_ale_p2", "k_b3h_g": "fct_ale_b3_horizontal",
-         "k_b3h_u": "fct_ale_b3_horizontal", "k_p2f": "fct_ale_p2_b3h"}
+NAMES = {"k_p1": "fct_ale_p1", "k_p1v": "fct_ale_p1v", "k_p2": "fct_ale_p2", "k_p2h": "fct_ale_p2h",
+         "k_b3h_g": "fct_ale_b3_horizontal", "k_b3h_u": "fct_ale_b3_horizontal", "k_p2f": "fct_ale_p2_b3h"}
+
+
+def kernel_key(name):
+    """rocprof kernel name -> short name; k_p1<..., VERT = true> is the phase-1 + vertical kernel."""
+    base = name.split("(")[0].replace("void ", "").replace("f2a::", "").strip()
+    k = base.split("<")[0]
+    if k == "k_p1" and base.rstrip(">").split(",")[-1].strip() == "true":
+        return "k_p1v"
+    return k
 
 
 def per_kernel(path):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("f2a::", "").strip()
+        k = kernel_key(r["Kernel_Name"])
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
