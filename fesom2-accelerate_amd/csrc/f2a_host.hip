@@ -501,13 +501,15 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             pedges.insert(pedges.end(), refs.begin() + ptr[n], refs.begin() + ptr[n + 1]);
             ni.e1 = (int)pedges.size();
             ni.r0 = (int)pring.size();
-            if (with_ring) pring.insert(pring.end(), ring.begin() + rptr[n], ring.begin() + rptr[n + 1]);
-            ni.r1 = (int)pring.size();
-            ni.zdry = with_ring ? zdry[n] : 0;
             ni.self_lev = 0;
-            if (with_ring)
+            if (with_ring) {  // the node itself last (k_p1 takes it from its own column, see RingRef)
                 for (int r = rptr[n]; r < rptr[n + 1]; r++)
                     if (ring[r].node == n) ni.self_lev = ring[r].lev;
+                    else pring.push_back(ring[r]);
+                pring.push_back(RingRef{n, ni.self_lev});
+            }
+            ni.r1 = (int)pring.size();
+            ni.zdry = with_ring ? zdry[n] : 0;
         }
         // edges in the order of their first visited endpoint (edges without an owned endpoint last)
         std::vector<int4> einfo;

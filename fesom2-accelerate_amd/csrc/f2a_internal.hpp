@@ -35,6 +35,9 @@ struct EdgeRef {
 // One node of a node's cluster (the union of the nodes of its adjacent elements).  `lev` is the
 // number of levels on which the node takes part in the cluster bound:
 // max over adjacent elements e that contain it of (nlevels(e) - 1)  (reference.cpp:331, :363-377).
+// In the processing-order copies (MeshPlanDev::p_ring, NodeRec::ring) the node itself is the last
+// entry of its slice, with lev = NodeInfo::self_lev: k_p1 reads its own column once for the
+// cluster bound, b2 and the vertical tail, and gathers only [r0, r1 - 1).
 struct RingRef {
     int node;
     int lev;

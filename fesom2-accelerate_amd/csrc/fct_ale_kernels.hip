@@ -347,6 +347,9 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
 #pragma unroll
     for (int c = 0; c < C; c++) vx[c] = vn[c] = p[c] = m[c] = 0.;
     size_t b = 0, ab = 0;
+    real lo[C], tt[C];  // own LO / ttf
+#pragma unroll
+    for (int c = 0; c < C; c++) lo[c] = tt[c] = 0.;
     real v[C + 1];  // raw fct_adf_v at z0 .. z0+C (b1v; the VERT tail limits them)
 #pragma unroll
     for (int c = 0; c <= C; c++) v[c] = 0.;
@@ -368,8 +371,17 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
-        cluster_bound<C, RB>(recs[j].ring, 0, min(nr, kRecRing), a.LO, a.ttf, z0, L, vx, vn);
-        if (nr > kRecRing) cluster_bound<C, RB>(mp.p_ring, ni.r0 + kRecRing, ni.r1, a.LO, a.ttf, z0, L, vx, vn);
+        ldv<C>(a.LO + b, lo);  // the own column: cluster bound (self last in the ring), b2, cv
+        ldv<C>(a.ttf + b, tt);
+#pragma unroll
+        for (int c = 0; c < C; c++)
+            if (nr > 0 && z0 + c < ni.self_lev) {
+                vx[c] = RMAX(vx[c], RMAX(lo[c], tt[c]));
+                vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
+            }
+        const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
+        cluster_bound<C, RB>(recs[j].ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn);
+        if (no > kRecRing) cluster_bound<C, RB>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn);
         auto add = [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
@@ -393,11 +405,10 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     }
     __syncthreads();
     if (!VERT && nw == 0) return;
-    real lo[C], ai[C], op[C], om[C];
+    real ai[C], op[C], om[C];
 #pragma unroll
-    for (int c = 0; c < C; c++) lo[c] = ai[c] = op[c] = om[c] = 0.;
+    for (int c = 0; c < C; c++) ai[c] = op[c] = om[c] = 0.;
     if (nw > 0) {
-    ldv<C>(a.LO + b, lo);
 #pragma unroll
     for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
 #pragma unroll
@@ -482,9 +493,8 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         }
         real dv[C];
         if (nw > 0) {
-            real del_v[C], tt[C], hn[C], hnn[C];
+            real del_v[C], hn[C], hnn[C];
             ldv_s<C, NT>(a.del_v + b, del_v);
-            ldv<C>(a.ttf + b, tt);
             ldv_s<C, NT>(a.hnode + b, hn);
             ldv_s<C, NT>(a.hnode_new + b, hnn);
 #pragma unroll
