@@ -152,7 +152,9 @@ def build_local(args, rank, world):
     nx, ny, nl = global_dims(args, world)
     g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels, name=f"{args.config} x {world}")
     if world == 1:
-        return g, None
+        return (synth.permute_mesh(g) if args.permuted else g), None
+    if args.permuted:
+        raise SystemExit("--permuted is a single-GPU stress variant")
     part = partition.strip_parts(nx, ny, world)
     return partition.local_mesh(g, part, rank)  # (local mesh, halo lists)
 
@@ -185,12 +187,18 @@ def verify(args, e, step, m, fields, rank, world, dist):
     import oracle as O
     nx, ny, nl = global_dims(args, world)
     g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels)
+    if args.permuted:  # the oracle runs on the same numbering (sums follow the local edge order)
+        g = synth.permute_mesh(g)
+    npos = np.empty(g.N, np.int64)
+    npos[g.node_gid] = np.arange(g.N)
+    epos = np.empty(g.E, np.int64)
+    epos[g.edge_gid] = np.arange(g.E)
     wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
     bad = {}
     for k, fk in enumerate(synth.make_tracer_fields(g, ntr)):
         want = O.full_pass(g, fk)
         for p in parts:
-            gid = p["gid"]
+            gid = npos[p["gid"]]
             for name in ("plus", "minus"):
                 w = want[name].reshape(-1, L)[gid]
                 n = int(np.sum((p[name][k] != w) & wet[gid]))
@@ -200,7 +208,7 @@ def verify(args, e, step, m, fields, rank, world, dist):
                 n = int(np.sum(p[name][k] != want[name].reshape(-1, stride)[gid]))
                 if n:
                     bad[name] = bad.get(name, 0) + n
-            n = int(np.sum(p["adf_h"][k] != want["adf_h"].reshape(-1, L)[p["egid"]]))
+            n = int(np.sum(p["adf_h"][k] != want["adf_h"].reshape(-1, L)[epos[p["egid"]]]))
             if n:
                 bad["adf_h"] = bad.get("adf_h", 0) + n
     return {"exact": not bad, "mismatched_cells": bad, "tracers": ntr,
@@ -217,6 +225,8 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: the config per GPU; strong: the config split over the GPUs (SURVEY.md 8(e))")
     ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
+    ap.add_argument("--permuted", action="store_true",
+                    help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
     ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise"],

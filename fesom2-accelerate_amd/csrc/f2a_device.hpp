@@ -224,6 +224,24 @@ __device__ __forceinline__ void stv_s(real *__restrict__ p, const real (&v)[C], 
     }
 }
 
+// Columns of the stride-nl arrays (fct_adf_v, area, area_inv) start at 8-byte alignment only; a
+// 16-byte load at 8-byte alignment (legal on gfx950: the compiler emits global_load_dwordx4 for
+// it) halves their load instructions.  Both levels of a pair lie inside the column (z0 + 1 <= L <
+// nl), so the second is loaded even when only the first is wet; it is then replaced by `fill`.
+typedef double f2a_d2u __attribute__((ext_vector_type(2), aligned(8)));
+template <int C, bool PAIR>
+__device__ __forceinline__ void ld_nl(const real *__restrict__ p, int nw, real (&v)[C], real fill)
+{
+    if constexpr (PAIR && C == 2) {
+        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(p);
+        v[0] = t.x;
+        v[1] = nw >= 2 ? t.y : fill;
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; c++) v[c] = c < nw ? p[c] : fill;
+    }
+}
+
 template <bool NT>
 __device__ __forceinline__ real ld1_s(const real *__restrict__ p)
 {

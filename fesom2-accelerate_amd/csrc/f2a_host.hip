@@ -423,11 +423,31 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     // Nodes inside a patch keep ascending index order.  Results do not depend on the order: each
     // node's sums run over its own CSR in ascending edge order.
     if (n_csr == n_owned && n_owned > 0 && m.nlev_nod) {
+        // Patch order: a numbering with locality (median |n1 - n2| over the edges at most N/64, e.g.
+        // row-major or space-filling-curve numbered meshes) keeps ascending index order inside
+        // large patches -- adjacent positions are then adjacent in memory too; a scattered
+        // numbering gets Cuthill-McKee order inside smaller patches (measured).
+        bool local_numbering = true;
+        {
+            std::vector<int> gap;
+            gap.reserve(refs.size());
+            for (int n = 0; n < n_owned; n++)
+                for (int k = ptr[n]; k < ptr[n + 1]; k++) gap.push_back(std::abs(other[k] - n));
+            if (!gap.empty()) {
+                std::nth_element(gap.begin(), gap.begin() + gap.size() / 2, gap.end());
+                local_numbering = gap[gap.size() / 2] <= std::max(n_owned / 64, 64);
+            }
+        }
         const char *env = getenv("FESOM2_PATCH");
-        const int patch = env ? atoi(env) : 64;
+        const int patch = env ? atoi(env) : (local_numbering ? 16384 : 4096);
         const char *senv = getenv("FESOM2_SUBPATCH");
         const int sub = senv ? atoi(senv) : 0;
+        const char *oenv = getenv("FESOM2_PATCH_ORDER");
+        const int porder = oenv ? atoi(oenv) : (local_numbering ? 0 : 1);
         std::vector<int> order;
+        std::vector<int> stamp, bq;  // FESOM2_PATCH_ORDER = 1: patch membership stamps, BFS queue
+        if (porder == 1) stamp.assign(n_owned, -1);
+        int npatch = 0;
         order.reserve(n_owned);
         if (patch <= 1) {
             for (int n = 0; n < n_owned; n++) order.push_back(n);
@@ -452,7 +472,36 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     }
                 }
                 for (size_t h = cur.size(); h < queue.size(); h++) seen[queue[h]] = 0;  // back to the pool
-                std::sort(cur.begin(), cur.end());
+                if (porder == 1 && cur.size() > 2) {
+                    // Cuthill-McKee inside the patch from a peripheral node (the last node a BFS
+                    // from the seed reaches): the BFS level sets cut across the patch, so graph
+                    // neighbours sit at most about one patch width apart, whatever the numbering
+                    const int id = npatch;
+                    for (int v : cur) stamp[v] = id;
+                    auto bfs = [&](int root) {
+                        bq.assign(1, root);
+                        stamp[root] = id + n_owned;  // visited mark for this sweep
+                        for (size_t h = 0; h < bq.size(); h++)
+                            for (int k = ptr[bq[h]]; k < ptr[bq[h] + 1]; k++) {
+                                const int w = other[k];
+                                if (w < n_owned && stamp[w] == id) {
+                                    stamp[w] = id + n_owned;
+                                    bq.push_back(w);
+                                }
+                            }
+                        for (int v : bq) stamp[v] = id;
+                    };
+                    bfs(cur[0]);
+                    if (bq.size() == cur.size()) {
+                        bfs(bq.back());
+                        cur.assign(bq.begin(), bq.end());
+                    } else {
+                        std::sort(cur.begin(), cur.end());
+                    }
+                } else {
+                    std::sort(cur.begin(), cur.end());
+                }
+                npatch++;
                 if (sub > 1 && (int)cur.size() > sub) {
                     // FESOM2_SUBPATCH: cut the patch into compact BFS blobs of `sub` nodes (the
                     // fused kernels' columns per block), so a block's columns share their clusters

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // fct_adf_v is limited from the raw values the thread already holds and written after the barriers
 // (every raw fct_adf_v read of the block happened before the first one), and del_ttf_advvert is
 // updated -- the arithmetic of k_p2, so results are identical.
-template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false>
+template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
@@ -353,11 +353,21 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     real v[C + 1];  // raw fct_adf_v at z0 .. z0+C (b1v; the VERT tail limits them)
 #pragma unroll
     for (int c = 0; c <= C; c++) v[c] = 0.;
+    real ai[C], e_dv[C], e_hn[C], e_hnn[C], e_ar[C];  // area_inv; OPT & 2: the tail's own streams
+#pragma unroll
+    for (int c = 0; c < C; c++) ai[c] = e_dv[c] = e_hn[c] = e_hnn[c] = e_ar[c] = 0.;
     if (nw > 0) {
         b = (size_t)ni.n * L + z0;
         ab = (size_t)ni.n * a.nl + z0;
+        if constexpr ((OPT & 4) != 0 && C == 2) {
+            const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(a.adf_v + ab);  // one 16-B load at 8-B alignment
+            v[0] = t.x;
+            v[1] = t.y;
+            v[2] = nw == 2 ? a.adf_v[ab + 2] : 0.;
+        } else {
 #pragma unroll
         for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? ld1_s<NT>(a.adf_v + ab + c) : 0.;
+        }
 #pragma unroll
         for (int c = 0; c < C; c++) {
             p[c] = RMAX(0., v[c]) + RMAX(0., -v[c + 1]);  // b1-vertical, reference.cpp:393-399
@@ -373,6 +383,17 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         }
         ldv<C>(a.LO + b, lo);  // the own column: cluster bound (self last in the ring), b2, cv
         ldv<C>(a.ttf + b, tt);
+        if constexpr (OPT & 1) {
+            // OPT & 1: the own-column streams of b2 and the vertical tail are issued with the first
+            // loads, so they land during the gathers instead of after the barriers
+            ld_nl<C, (OPT & 4) != 0>(a.area_inv + ab, nw, ai, 0.);
+            if constexpr (VERT && (OPT & 2)) {
+                ldv<C>(a.del_v + b, e_dv);
+                ldv<C>(a.hnode + b, e_hn);
+                ldv<C>(a.hnode_new + b, e_hnn);
+                ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, e_ar, 1.);
+            }
+        }
 #pragma unroll
         for (int c = 0; c < C; c++)
             if (nr > 0 && z0 + c < ni.self_lev) {
@@ -382,6 +403,14 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
         cluster_bound<C, RB>(recs[j].ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn);
         if (no > kRecRing) cluster_bound<C, RB>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn);
+        if constexpr ((OPT & 2) && VERT) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                real tv = e_dv[c] - tt[c] * e_hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
+                e_dv[c] = tv + lo[c] * e_hnn[c];
+                e_ar[c] = a.dt / e_ar[c];
+            }
+        }
         auto add = [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
@@ -405,12 +434,16 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     }
     __syncthreads();
     if (!VERT && nw == 0) return;
-    real ai[C], op[C], om[C];
+    real op[C], om[C];
 #pragma unroll
-    for (int c = 0; c < C; c++) ai[c] = op[c] = om[c] = 0.;
+    for (int c = 0; c < C; c++) op[c] = om[c] = 0.;
     if (nw > 0) {
+    if constexpr (!(OPT & 1)) {
+        if constexpr ((OPT & 4) != 0) ld_nl<C, true>(a.area_inv + ab, nw, ai, 0.);
+        else
 #pragma unroll
-    for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
+        for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
+    }
 #pragma unroll
     for (int c = 0; c < C; c++) {
         op[c] = om[c] = 0.;
@@ -492,14 +525,19 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             lim[c] = lim_here ? b3v_factor(z, v[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) * v[c] : v[c];
         }
         real dv[C];
-        if (nw > 0) {
+        if ((OPT & 2) && nw > 0) {
+#pragma unroll
+            for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
+        } else if (nw > 0) {
             real del_v[C], hn[C], hnn[C];
             ldv_s<C, NT>(a.del_v + b, del_v);
             ldv_s<C, NT>(a.hnode + b, hn);
             ldv_s<C, NT>(a.hnode_new + b, hnn);
+            real ar[C];
+            ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
             for (int c = 0; c < C; c++) {
-                const real dta = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+                const real dta = c < nw ? a.dt / ar[c] : 0.;
                 real tv = del_v[c] - tt[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
                 tv = tv + lo[c] * hnn[c];
                 dv[c] = tv + (lim[c] - lim[c + 1]) * dta;
@@ -507,13 +545,21 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         }
 #pragma unroll
         for (int c = 0; c < C; c++)
-            if (c < na) st1_s<NT>(const_cast<real *>(a.adf_v) + ab + c, lim[c]);  // limited in place
+            if (!((OPT & 4) != 0 && C == 2 && na == 2) && c < na)
+                st1_s<NT>(const_cast<real *>(a.adf_v) + ab + c, lim[c]);  // limited in place
+        if constexpr ((OPT & 4) != 0 && C == 2)
+            if (na == 2) {
+                f2a_d2u t;
+                t.x = lim[0];
+                t.y = lim[1];
+                *reinterpret_cast<f2a_d2u *>(const_cast<real *>(a.adf_v) + ab) = t;
+            }
         if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
     }
 }
 
 // Phase 2, horizontal half (after the exchange, with b3h): c-horizontal only (see k_p1 VERT).
-template <int C, int KB, bool NT>
+template <int C, int KB, bool NT, bool PAIR = false>
 __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // NodeRec[G]
@@ -536,8 +582,15 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     const size_t b = (size_t)ni.n * L + z0, ab = (size_t)ni.n * a.nl + z0;
     real dh[C], dta[C];
     ldv_s<C, NT>(a.del_h + b, dh);
+    if constexpr (PAIR && C == 2) {  // area: one 16-B load at 8-B alignment (ld_nl)
+        const f2a_d2u t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2a_d2u *>(a.area + ab))
+                             : *reinterpret_cast<const f2a_d2u *>(a.area + ab);
+        dta[0] = a.dt / t.x;
+        dta[1] = nw >= 2 ? a.dt / t.y : 0.;
+    } else {
 #pragma unroll
-    for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+        for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+    }
     const int ne = ni.e1 - ni.e0;
     auto add = [&](int c, real h, int second) {
         dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
@@ -957,9 +1010,16 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const float invS = 1.0f / (float)S;
     const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
     if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
+    // OPT bits of k_p1 (VERT): 1 area_inv issued with the first loads, 2 + the tail's own streams
+    // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default)
+    const int early = env_int("FESOM2_P1V_EARLY", 0) | (env_int("FESOM2_NL_PAIR", 1) ? 4 : 0);
     if (C == 2) {
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early == 1) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 1>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early == 5) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 5>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early & 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 7>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -974,8 +1034,11 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
     const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;
+    const bool pair = env_int("FESOM2_NL_PAIR", 1) != 0;  // 16-B loads of the stride-nl area (ld_nl)
     if (C == 2) {
+        if (NT && pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p2h<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
     if (NT) F2A_LAUNCH_GROUPS((k_p2h<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
