@@ -27,7 +27,8 @@ def kernel_key(name):
     """rocprof kernel name -> short name; k_p1<..., VERT = true> is the phase-1 + vertical kernel."""
     base = name.split("(")[0].replace("void ", "").replace("f2a::", "").strip()
     k = base.split("<")[0]
-    if k == "k_p1" and base.rstrip(">").split(",")[-1].strip() == "true":
+    args = [x.strip() for x in base[len(k) + 1:].rstrip(">").split(",")] if "<" in base else []
+    if k == "k_p1" and len(args) > 5 and args[5] == "true":  # k_p1<VLIMIT, C, RB, EB, NT, VERT, OPT>
         return "k_p1v"
     return k
 
