@@ -150,7 +150,12 @@ __device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false
 }
 
 
-// C consecutive levels; C even reads 16-byte pairs (p 16-byte aligned)
+// 16-byte pair of levels.  Columns of odd-L arrays and of the stride-nl arrays start at 8-byte
+// alignment only; a 16-byte load/store at 8-byte alignment is legal on gfx950 (the compiler emits
+// the same global_load_dwordx4 / global_store_dwordx4 it emits for 16-byte alignment).
+typedef double f2a_d2u __attribute__((ext_vector_type(2), aligned(8)));
+
+// C consecutive levels; C even reads 16-byte pairs (p 8-byte aligned)
 template <int C>
 __device__ __forceinline__ void ldv(const real *__restrict__ p, real (&v)[C])
 {
@@ -159,7 +164,7 @@ __device__ __forceinline__ void ldv(const real *__restrict__ p, real (&v)[C])
     } else {
 #pragma unroll
         for (int c = 0; c < C; c += 2) {
-            const double2 t = *reinterpret_cast<const double2 *>(p + c);
+            const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(p + c);
             v[c] = t.x;
             v[c + 1] = t.y;
         }
@@ -175,17 +180,21 @@ __device__ __forceinline__ void stv(real *__restrict__ p, const real (&v)[C], in
     } else {
 #pragma unroll
         for (int c = 0; c < C; c += 2) {
-            if (c + 2 <= n)
-                *reinterpret_cast<double2 *>(p + c) = make_double2(v[c], v[c + 1]);
-            else if (c < n)
+            if (c + 2 <= n) {
+                f2a_d2u t;
+                t.x = v[c];
+                t.y = v[c + 1];
+                *reinterpret_cast<f2a_d2u *>(p + c) = t;
+            } else if (c < n) {
                 p[c] = v[c];
+            }
         }
     }
 }
 
 // Single-use streams (a column nobody else reads in the same kernel) can bypass the L2 with
 // non-temporal loads/stores, leaving it to the gathered columns.
-typedef double f2a_d2 __attribute__((ext_vector_type(2)));
+typedef f2a_d2u f2a_d2;
 template <int C, bool NT>
 __device__ __forceinline__ void ldv_s(const real *__restrict__ p, real (&v)[C])
 {
@@ -224,11 +233,37 @@ __device__ __forceinline__ void stv_s(real *__restrict__ p, const real (&v)[C], 
     }
 }
 
+// Odd L in pairs (C = 2, S = (L+1)/2 slots per column): the last slot of a column holds the one
+// level z0 = L-1 (`last1`).  Its pair load starts one level earlier, inside the column, and keeps the
+// upper value, so no load reaches into the next column or past the end of an array.
+template <int C, bool ODD>
+__device__ __forceinline__ void ldo(const real *__restrict__ p, real (&v)[C], bool last1)
+{
+    if constexpr (ODD && C == 2) {
+        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(last1 ? p - 1 : p);
+        v[0] = last1 ? t.y : t.x;
+        v[1] = last1 ? 0. : t.y;
+    } else {
+        ldv<C>(p, v);
+    }
+}
+template <int C, bool NT, bool ODD>
+__device__ __forceinline__ void ldo_s(const real *__restrict__ p, real (&v)[C], bool last1)
+{
+    if constexpr (ODD && C == 2) {
+        const f2a_d2u *q = reinterpret_cast<const f2a_d2u *>(last1 ? p - 1 : p);
+        const f2a_d2u t = NT ? __builtin_nontemporal_load(q) : *q;
+        v[0] = last1 ? t.y : t.x;
+        v[1] = last1 ? 0. : t.y;
+    } else {
+        ldv_s<C, NT>(p, v);
+    }
+}
+
 // Columns of the stride-nl arrays (fct_adf_v, area, area_inv) start at 8-byte alignment only; a
 // 16-byte load at 8-byte alignment (legal on gfx950: the compiler emits global_load_dwordx4 for
 // it) halves their load instructions.  Both levels of a pair lie inside the column (z0 + 1 <= L <
 // nl), so the second is loaded even when only the first is wet; it is then replaced by `fill`.
-typedef double f2a_d2u __attribute__((ext_vector_type(2), aligned(8)));
 template <int C, bool PAIR>
 __device__ __forceinline__ void ld_nl(const real *__restrict__ p, int nw, real (&v)[C], real fill)
 {
@@ -259,11 +294,11 @@ __device__ __forceinline__ void st1_s(real *__restrict__ p, real v)
 // straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
 // (vx, vn must be initialised by the caller: -/+bignumber where an adjacent element is dry, else
 // -/+infinity)
-template <int C, int kBatch>
+template <int C, int kBatch, bool ODD = false>
 __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, int r0, int r1,
                                               const real *__restrict__ LO,
                                               const real *__restrict__ ttf, int z0, int L,
-                                              real (&vx)[C], real (&vn)[C])
+                                              real (&vx)[C], real (&vn)[C], bool last1 = false)
 {
     for (int r = r0; r < r1; r += kBatch) {
         size_t idx[kBatch];
@@ -278,8 +313,8 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             if (z0 < lev[k]) {
-                ldv<C>(LO + idx[k], lo[k]);
-                ldv<C>(ttf + idx[k], tt[k]);
+                ldo<C, ODD>(LO + idx[k], lo[k], last1);
+                ldo<C, ODD>(ttf + idx[k], tt[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) lo[k][c] = tt[k][c] = 0.;
@@ -306,9 +341,10 @@ __device__ __forceinline__ void ldv_coh(const real *p, real (&v)[C])
     for (int c = 0; c < C; c++) v[c] = __hip_atomic_load(p + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int C, int kBatch, bool COH = false, class F>
+template <int C, int kBatch, bool COH = false, bool ODD = false, class F>
 __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
-                                          const real *__restrict__ adf_h, int z0, int L, F &&f)
+                                          const real *__restrict__ adf_h, int z0, int L, F &&f,
+                                          bool last1 = false)
 {
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
         size_t idx[kBatch];
@@ -326,7 +362,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
                 if constexpr (COH)
                     ldv_coh<C>(adf_h + idx[k], h[k]);
                 else
-                    ldv<C>(adf_h + idx[k], h[k]);
+                    ldo<C, ODD>(adf_h + idx[k], h[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;
@@ -359,15 +395,16 @@ __device__ __forceinline__ const NodeRec *stage_records(const NodeRec *__restric
 // the grid has U times fewer blocks.  NT: fct_adf_h streamed with non-temporal loads/stores so the
 // gathered plus/minus columns keep the L2.
 // U edge groups starting at group `ug` (relative to einfo) of one tracer.
-template <int C, int U, bool NT>
+template <int C, int U, bool NT, bool ODD = false>
 __device__ __forceinline__ void b3h_groups(const int4 *__restrict__ einfo, int n_edges, int L, int G, float invS,
                                            const real *__restrict__ plus, const real *__restrict__ minus,
                                            real *__restrict__ adf_h, int ug)
 {
     int j, u;
-    slot_of(threadIdx.x, L / C, invS, j, u);
+    slot_of(threadIdx.x, (L + C - 1) / C, invS, j, u);
     if (j >= G) return;
     const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
     const int k0 = ug * U * G + j;
     int4 ei[U];
 #pragma unroll
@@ -379,12 +416,12 @@ __device__ __forceinline__ void b3h_groups(const int4 *__restrict__ einfo, int n
 #pragma unroll
     for (int q = 0; q < U; q++) {
         if (z0 < ei[q].z) {
-            ldv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, f[q]);
+            ldo_s<C, NT, ODD>(adf_h + (size_t)ei[q].w * L + z0, f[q], last1);
             const size_t i1 = (size_t)ei[q].x * L + z0, i2 = (size_t)ei[q].y * L + z0;
-            ldv<C>(plus + i1, p1[q]);
-            ldv<C>(minus + i1, m1[q]);
-            ldv<C>(plus + i2, p2[q]);
-            ldv<C>(minus + i2, m2[q]);
+            ldo<C, ODD>(plus + i1, p1[q], last1);
+            ldo<C, ODD>(minus + i1, m1[q], last1);
+            ldo<C, ODD>(plus + i2, p2[q], last1);
+            ldo<C, ODD>(minus + i2, m2[q], last1);
         }
     }
 #pragma unroll

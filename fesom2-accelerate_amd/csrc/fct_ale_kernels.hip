@@ -316,11 +316,11 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // fct_adf_v is limited from the raw values the thread already holds and written after the barriers
 // (every raw fct_adf_v read of the block happened before the first one), and del_ttf_advvert is
 // updated -- the arithmetic of k_p2, so results are identical.
-template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0>
+template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
-    const int L = a.nl - 1, S = L / C;
+    const int L = a.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
     int tr;
     const int first = group_tracer(a.tr.n, tr, c_tracer_major & 1) * G;
@@ -338,6 +338,7 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     int j, u;
     slot_of(t, S, invS, j, u);
     const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
     const bool col = j < ncol;
     NodeInfo ni{};
     if (col) ni = recs[j].info;
@@ -381,16 +382,16 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
-        ldv<C>(a.LO + b, lo);  // the own column: cluster bound (self last in the ring), b2, cv
-        ldv<C>(a.ttf + b, tt);
+        ldo<C, ODD>(a.LO + b, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
+        ldo<C, ODD>(a.ttf + b, tt, last1);
         if constexpr (OPT & 1) {
             // OPT & 1: the own-column streams of b2 and the vertical tail are issued with the first
             // loads, so they land during the gathers instead of after the barriers
             ld_nl<C, (OPT & 4) != 0>(a.area_inv + ab, nw, ai, 0.);
             if constexpr (VERT && (OPT & 2)) {
-                ldv<C>(a.del_v + b, e_dv);
-                ldv<C>(a.hnode + b, e_hn);
-                ldv<C>(a.hnode_new + b, e_hnn);
+                ldo<C, ODD>(a.del_v + b, e_dv, last1);
+                ldo<C, ODD>(a.hnode + b, e_hn, last1);
+                ldo<C, ODD>(a.hnode_new + b, e_hnn, last1);
                 ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, e_ar, 1.);
             }
         }
@@ -401,8 +402,9 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
                 vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
             }
         const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
-        cluster_bound<C, RB>(recs[j].ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn);
-        if (no > kRecRing) cluster_bound<C, RB>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn);
+        cluster_bound<C, RB, ODD>(recs[j].ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
+        if (no > kRecRing)
+            cluster_bound<C, RB, ODD>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn, last1);
         if constexpr ((OPT & 2) && VERT) {
 #pragma unroll
             for (int c = 0; c < C; c++) {
@@ -420,17 +422,18 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
                 m[c] += RMIN(0., h);
             }
         };
-        for_edges<C, EB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
-        if (ne > kRecEdge) for_edges<C, EB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+        for_edges<C, EB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+        if (ne > kRecEdge) for_edges<C, EB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     }
     real *tvx = lds, *tvn = lds + G * L;
     const int q = j * L + z0;
     if (col) {
 #pragma unroll
-        for (int c = 0; c < C; c++) {
-            tvx[q + c] = vx[c];
-            tvn[q + c] = vn[c];
-        }
+        for (int c = 0; c < C; c++)
+            if (!ODD || c == 0 || !last1) {  // ODD: the last slot's second level is the next column's
+                tvx[q + c] = vx[c];
+                tvn[q + c] = vn[c];
+            }
     }
     __syncthreads();
     if (!VERT && nw == 0) return;
@@ -491,10 +494,11 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         real *pl = lds, *mn = lds + G * L;
         if (col) {
 #pragma unroll
-            for (int c = 0; c < C; c++) {
-                pl[q + c] = op[c];
-                mn[q + c] = om[c];
-            }
+            for (int c = 0; c < C; c++)
+                if (!ODD || c == 0 || !last1) {
+                    pl[q + c] = op[c];
+                    mn[q + c] = om[c];
+                }
         }
         __syncthreads();
         const int top = Ln > 1 ? Ln : 1;                   // the Fortran always limits nz = 1
@@ -530,9 +534,9 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
         } else if (nw > 0) {
             real del_v[C], hn[C], hnn[C];
-            ldv_s<C, NT>(a.del_v + b, del_v);
-            ldv_s<C, NT>(a.hnode + b, hn);
-            ldv_s<C, NT>(a.hnode_new + b, hnn);
+            ldo_s<C, NT, ODD>(a.del_v + b, del_v, last1);
+            ldo_s<C, NT, ODD>(a.hnode + b, hn, last1);
+            ldo_s<C, NT, ODD>(a.hnode_new + b, hnn, last1);
             real ar[C];
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
@@ -559,11 +563,11 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
 }
 
 // Phase 2, horizontal half (after the exchange, with b3h): c-horizontal only (see k_p1 VERT).
-template <int C, int KB, bool NT, bool PAIR = false>
+template <int C, int KB, bool NT, bool PAIR = false, bool ODD = false>
 __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, float invS)
 {
     extern __shared__ real lds[];  // NodeRec[G]
-    const int L = a.nl - 1, S = L / C;
+    const int L = a.nl - 1, S = (L + C - 1) / C;
     int tr;
     const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
     if (tr) {
@@ -575,13 +579,14 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     int j, u;
     slot_of(threadIdx.x, S, invS, j, u);
     const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
     if (j >= ncol) return;
     const NodeInfo ni = recs[j].info;
     const int nw = max(0, min(C, ni.Ln - z0));
     if (nw <= 0) return;
     const size_t b = (size_t)ni.n * L + z0, ab = (size_t)ni.n * a.nl + z0;
     real dh[C], dta[C];
-    ldv_s<C, NT>(a.del_h + b, dh);
+    ldo_s<C, NT, ODD>(a.del_h + b, dh, last1);
     if constexpr (PAIR && C == 2) {  // area: one 16-B load at 8-B alignment (ld_nl)
         const f2a_d2u t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2a_d2u *>(a.area + ab))
                              : *reinterpret_cast<const f2a_d2u *>(a.area + ab);
@@ -595,8 +600,8 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     auto add = [&](int c, real h, int second) {
         dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
     };
-    for_edges<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
-    if (ne > kRecEdge) for_edges<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+    for_edges<C, KB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+    if (ne > kRecEdge) for_edges<C, KB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
@@ -632,7 +637,7 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 }
 
 
-template <int C, int U, bool NT>
+template <int C, int U, bool NT, bool ODD = false>
 __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, int n_edges, int L,
                                                 int G, float invS, const real *__restrict__ plus,
                                                 const real *__restrict__ minus,
@@ -640,8 +645,8 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
 {
     int tr;
     const int ug = group_tracer(trs.n, tr, c_tracer_major & 2);
-    b3h_groups<C, U, NT>(einfo, n_edges, L, G, invS, plus + tr * trs.node, minus + tr * trs.node,
-                         adf_h + tr * trs.edge, ug);
+    b3h_groups<C, U, NT, ODD>(einfo, n_edges, L, G, invS, plus + tr * trs.node, minus + tr * trs.node,
+                              adf_h + tr * trs.edge, ug);
 }
 
 
@@ -1003,9 +1008,21 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     }
 }
 
+// odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0: one level
+// per thread)
+static bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && env_int("FESOM2_ODD_PAIR", 1) != 0; }
+
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = a.nl - 1;
+    if (odd_pairs(L) && a.vlimit == 1) {
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+        if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
+    }
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
@@ -1029,7 +1046,17 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 
 hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = a.nl - 1;
+    if (odd_pairs(L)) {
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+        const size_t lds = (size_t)G * sizeof(NodeRec);
+        const float invS = 1.0f / (float)S;
+        if ((env_int("FESOM2_NT", 2) & 2) != 0)
+            F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1077,6 +1104,12 @@ hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus,
                             real *adf_h, const Tracers &tr, hipStream_t s)
 {
     const int L = nl - 1;
+    if (odd_pairs(L)) {
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long ug = ((count + G - 1) / G + 1) / 2 * tr.n;  // two edge groups per block
+        F2A_LAUNCH_GROUPS((k_b3h_u<2, 2, true, true>), ug, G, S, 0, s, ei, count, L, G, 1.0f / (float)S, plus, minus,
+                          adf_h, tr);
+    }
     int C = levels_per_thread(L);
     if (C == 2 && L % 4 == 0 && env_int("FESOM2_B3H_CPT", 2) == 4) C = 4;  // 4 levels: 2 x 16 B per array
     const int S = L / C, G = group_columns(S);
