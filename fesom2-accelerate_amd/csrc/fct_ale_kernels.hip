@@ -357,9 +357,24 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     real ai[C], e_dv[C], e_hn[C], e_hnn[C], e_ar[C];  // area_inv; OPT & 2: the tail's own streams
 #pragma unroll
     for (int c = 0; c < C; c++) ai[c] = e_dv[c] = e_hn[c] = e_hnn[c] = e_ar[c] = 0.;
+    // OPT & 8 (VERT, even L): the vertical tail's own L-stride streams (del_ttf_advvert, hnode,
+    // hnode_new) go global -> LDS by DMA (global_load_lds_dwordx4, no VGPRs) right after the records,
+    // lane-linear behind the NodeRecs; the first barrier's vmcnt(0) lands them
+    real *gl = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real));
+    const int gl_n = (int)blockDim.x * C;  // doubles per DMA region
     if (nw > 0) {
         b = (size_t)ni.n * L + z0;
         ab = (size_t)ni.n * a.nl + z0;
+        if constexpr (VERT && (OPT & 8) && C == 2 && !ODD) {
+            auto dma = [&](const real *src, real *dst) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+            };
+            real *w = gl + (threadIdx.x >> 6) * 64 * C;  // wave base: lane i lands at w + C*i
+            dma(a.del_v + b, w);
+            dma(a.hnode + b, w + gl_n);
+            dma(a.hnode_new + b, w + 2 * gl_n);
+        }
         if constexpr ((OPT & 4) != 0 && C == 2) {
             const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(a.adf_v + ab);  // one 16-B load at 8-B alignment
             v[0] = t.x;
@@ -534,9 +549,19 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
         } else if (nw > 0) {
             real del_v[C], hn[C], hnn[C];
-            ldo_s<C, NT, ODD>(a.del_v + b, del_v, last1);
-            ldo_s<C, NT, ODD>(a.hnode + b, hn, last1);
-            ldo_s<C, NT, ODD>(a.hnode_new + b, hnn, last1);
+            if constexpr ((OPT & 8) && C == 2 && !ODD) {
+                const real *me = gl + C * threadIdx.x;
+#pragma unroll
+                for (int c = 0; c < C; c++) {
+                    del_v[c] = me[c];
+                    hn[c] = me[gl_n + c];
+                    hnn[c] = me[2 * gl_n + c];
+                }
+            } else {
+                ldo_s<C, NT, ODD>(a.del_v + b, del_v, last1);
+                ldo_s<C, NT, ODD>(a.hnode + b, hn, last1);
+                ldo_s<C, NT, ODD>(a.hnode_new + b, hnn, last1);
+            }
             real ar[C];
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
@@ -1036,6 +1061,10 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (early == 1) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 1>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 5) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 5>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early == 12) {
+            const size_t lds_dma = lds + 3 * (size_t)threads_for(G, S) * 2 * sizeof(real);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 12>), groups, G, S, lds_dma, s, mp, a, G, invS);
+        }
         if (early & 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 7>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
     }

@@ -396,16 +396,52 @@ def test_sizes_beyond_int32():
     dll().fesom2_free_(h8.ref)
 
 
-@pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129, 200])
+def run_split(m, f):
+    """The direction-split pass (bench default): fct_ale_pre_comm_v_acc_ -> fct_ale_post_comm_h_acc_."""
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        return {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        e.free()
+        dm.free()
+
+
+@pytest.mark.parametrize("nl", [3, 4, 5, 6, 48, 81, 129, 200])
 @pytest.mark.parametrize("full", [False, True])
-def test_level_counts(nl, full):
+@pytest.mark.parametrize("split", [False, True])
+def test_level_counts(nl, full, split):
     """Level counts from the minimum to deep columns, odd and even L (one or two levels per thread,
-    columns per block from 1 to 64, 80-level columns and 128/199-level ones)."""
+    odd L in pairs with a one-level last slot on the split path, columns per block from 1 to 64,
+    80-level columns and 128/199-level ones)."""
     m = synth.make_mesh(40, 14, nl, full_depth=full)
     f = synth.make_fields(m)
-    st, got = run_pass(m, f)
-    assert st == 9
+    if split:
+        got = run_split(m, f)
+    else:
+        st, got = run_pass(m, f)
+        assert st == 9
     check_pass(m, got, O.full_pass(m, f))
+
+
+SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1V_EARLY": "8"},
+               {"FESOM2_ODD_PAIR": "0"}, {"FESOM2_NL_PAIR": "0"}, {"FESOM2_NL_PAIR": "0", "FESOM2_NT": "0"},
+               {"FESOM2_PATCH_ORDER": "1"}, {"FESOM2_PATCH_ORDER": "1", "FESOM2_PATCH": "100"},
+               {"FESOM2_PATCH_ORDER": "0", "FESOM2_PATCH": "64"}]
+
+
+@pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("name,perm", [("8k x 20", False), ("8k x 20", True), ("127k x 47", False)])
+def test_split_variants_match_oracle(knobs, name, perm, monkeypatch):
+    """The direction-split kernels' switches (p1v load placement, LDS-DMA tail, odd-L pairs,
+    16-byte stride-nl loads, processing orders) are all exact."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    m, f = mesh(name, False, perm)
+    check_pass(m, run_split(m, f), O.full_pass(m, f))
 
 
 @pytest.mark.parametrize("name,full,perm", CASES + [("tiny", True, False)])
