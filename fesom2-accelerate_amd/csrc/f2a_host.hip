@@ -578,7 +578,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             if (!etaken[e]) push_edge(e);
         // edges in owner order (chunked phase 2: an edge belongs to its first visited endpoint)
         d.p_edge_owner = plan->mem.upload(einfo);
-        if (!d.p_edge_owner) return fail("device allocation for the edge order failed");
+        d.p_owner_cum = plan->mem.upload(plan->owner_cum);
+        if (!d.p_edge_owner || !d.p_owner_cum) return fail("device allocation for the edge order failed");
         // persistent phase-2 plan (MeshPlanDev::wf_*): tiles of the fused kernels' G positions
         {
             const int WG = f2a::fused_group_columns(nl);

@@ -90,6 +90,7 @@ struct MeshPlanDev {
                                           // interior edges (both endpoints owned) first
     int n_edge_interior = 0;
     const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
+    const int *p_owner_cum = nullptr;     // [n_owned + 1]: edges owned by processing positions < k
     // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of
     // consecutive tiles; per tile the owned edges in wf_edges[wf_edge_ptr[t] ..), the earlier tiles
     // whose edges it needs in wf_deps[wf_dep_ptr[t] ..); edges between streams pre-limited (wf_cross)
@@ -173,6 +174,10 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
 // chunk c's node kernel and the next chunk's b3h in one launch (node blocks first; one tracer)
 hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int4 *einfo, int n_edges, hipStream_t s);
 // the same over an explicit edge list
+// b3-horizontal node-centric: the edges each processing position owns (p_edge_owner), the owner's
+// plus/minus loaded once for all of them; edges without an owned endpoint edge-centric
+hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
+                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
 hipError_t launch_b3h_edges(const int4 *einfo, int count, int nl, const real *plus, const real *minus,
                             real *adf_h, const Tracers &tr, hipStream_t s);
 // iter_yn phase 2 (docs/refactoring.md:227-229, :258-260, :265-290): node kernel = b3v writing

@@ -675,6 +675,63 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
 }
 
 
+// b3-horizontal, node-centric: column j of the block is processing position k and limits the edges
+// k owns (first visited endpoint, MeshPlanDev::p_edge_owner[p_owner_cum[k] ..)), all incident to
+// its node n: n's plus/minus are loaded once, per edge only fct_adf_h (non-temporal) and the other
+// endpoint's plus/minus -- 3 loads per edge instead of 5.  Every edge is written once, by its
+// owner, and read by nobody else in the launch.  Same b3h_factor arithmetic as k_b3h_u.
+template <int C, int EB, bool NT, bool ODD>
+__global__ __launch_bounds__(1024) void k_b3h_n(const NodeInfo *__restrict__ info, const int *__restrict__ owner_cum,
+                                                const int4 *__restrict__ eown, int n_pos, int L, int G, float invS,
+                                                const real *__restrict__ plus, const real *__restrict__ minus,
+                                                real *__restrict__ adf_h, Tracers trs)
+{
+    int tr;
+    const int first = group_tracer(trs.n, tr, c_tracer_major & 2) * G;
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
+    int j, u;
+    slot_of(threadIdx.x, (L + C - 1) / C, invS, j, u);
+    const int k = first + j;
+    if (j >= G || k >= n_pos) return;
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    const int e0 = owner_cum[k], e1 = owner_cum[k + 1];
+    if (e0 >= e1) return;
+    const int n = info[k].n;
+    real po[C], mo[C];
+    ldo<C, ODD>(plus + (size_t)n * L + z0, po, last1);
+    ldo<C, ODD>(minus + (size_t)n * L + z0, mo, last1);
+    for (int q0 = e0; q0 < e1; q0 += EB) {
+        int4 ei[EB];
+#pragma unroll
+        for (int q = 0; q < EB; q++) ei[q] = q0 + q < e1 ? eown[q0 + q] : make_int4(0, 0, 0, 0);
+        real f[EB][C], px[EB][C], mx[EB][C];
+#pragma unroll
+        for (int q = 0; q < EB; q++) {
+            if (z0 < ei[q].z) {
+                const int o = ei[q].x == n ? ei[q].y : ei[q].x;
+                ldo_s<C, NT, ODD>(adf_h + (size_t)ei[q].w * L + z0, f[q], last1);
+                ldo<C, ODD>(plus + (size_t)o * L + z0, px[q], last1);
+                ldo<C, ODD>(minus + (size_t)o * L + z0, mx[q], last1);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < EB; q++) {
+            const int nw = min(C, ei[q].z - z0);
+            if (nw <= 0) continue;
+            const bool own_first = ei[q].x == n;  // node1 of the edge (docs/refactoring.md:246-257)
+            real out[C];
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                out[c] = (own_first ? b3h_factor(f[q][c], po[c], mo[c], px[q][c], mx[q][c])
+                                    : b3h_factor(f[q][c], px[q][c], mx[q][c], po[c], mo[c])) * f[q][c];
+            stv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, out, nw);
+        }
+    }
+}
+
 template <int C, int KB, bool NT>
 __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
@@ -1121,6 +1178,38 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
+                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
+{
+    const int L = nl - 1, N = mp.n_owned;
+    if (!mp.p_owner_cum || !mp.node_info) return hipErrorInvalidValue;
+    const bool odd = L % 2 == 1;
+    const int C = (L % 2 == 0 || odd_pairs(L)) ? 2 : 1;
+    const int S = (L + C - 1) / C, G = group_columns(S);
+    const long groups = (long)(N + G - 1) / G * tr.n;
+    const float invS = 1.0f / (float)S;
+    const int EB = env_int("FESOM2_B3HN_EB", 2);
+    auto go = [&]() -> hipError_t {
+        if (C == 2 && !odd) {
+            if (EB == 1) F2A_LAUNCH_GROUPS((k_b3h_n<2, 1, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+            if (EB == 3) F2A_LAUNCH_GROUPS((k_b3h_n<2, 3, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+        }
+        if (C == 2)
+            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, true>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+        F2A_LAUNCH_GROUPS((k_b3h_n<1, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                          mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+    };
+    const hipError_t e = go();
+    if (e != hipSuccess || owned_edges >= n_edges) return e;
+    // edges without an owned endpoint (none in a FESOM partition): edge-centric
+    return launch_b3h_edges(mp.p_edge_owner + owned_edges, n_edges - owned_edges, nl, plus, minus, adf_h, tr, s);
 }
 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,

@@ -641,6 +641,7 @@ hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t
         if (C == 2) {
             if (EB == 1) { F2A_P1E(2, 1) }
             if (EB == 4) { F2A_P1E(2, 4) }
+            if (EB == 3) { F2A_P1E(2, 3) }
             F2A_P1E(2, 2)
         }
         F2A_P1E(1, 2)
