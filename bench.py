@@ -229,9 +229,10 @@ def main():
                     help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
-    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise"],
+    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference"],
                     help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
-                         "stepwise: one kernel per reference step")
+                         "stepwise: one kernel per reference step; reference: the reference's entry sequence "
+                         "pre_comm -> inter_comm -> post_comm -> c with the fused phase 1")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
     ap.add_argument("--check", action="store_true",
@@ -280,7 +281,7 @@ def main():
 
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
-    if args.tracers > 1 and args.path == "stepwise":
+    if args.tracers > 1 and args.path in ("stepwise", "reference"):
         raise SystemExit("--tracers > 1 runs the batched (fused or split) entry points only")
     fields = synth.make_tracer_fields(m, args.tracers)
     f = fields[0]
@@ -339,7 +340,7 @@ def main():
         if world > 1 and args.exchange == "host":
             host_exchange()
             s2 = e.post_comm_c() if args.path == "fused" else (e.inter_comm(), e.post_comm(), e.c_step())[-1]
-        elif args.path == "stepwise":
+        elif args.path in ("stepwise", "reference"):
             if halo is not None:
                 e.exchange(halo.comm, halo.plan)
             s2 = (e.inter_comm(), e.post_comm(), e.c_step())[-1]
@@ -432,6 +433,13 @@ def main():
                "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
                          f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)",
                "all_cores": cpu_all, "host": host_info()}
+        t_ref = O.time_ref_pre_comm(m, f)
+        if t_ref is not None:
+            cpu["reference_phase1"] = {
+                "value": round(s["cn"] / t_ref, 1), "unit": "cell-updates/s", "cores": 1, "kind": "reference",
+                "sample": f"src/reference.cpp fct_ale_a1..a4_reference_ (a1..b2, all the reference runs on the CPU; "
+                          f"built from /root/reference by oracle/Makefile), same {args.config} mesh, single thread, "
+                          f"best of 2 ({t_ref:.2f} s per phase 1)"}
 
     check = None
     if args.check:

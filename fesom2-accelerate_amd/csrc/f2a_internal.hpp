@@ -176,6 +176,11 @@ hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int
 // the same over an explicit edge list
 // b3-horizontal node-centric: the edges each processing position owns (p_edge_owner), the owner's
 // plus/minus loaded once for all of them; edges without an owned endpoint edge-centric
+// reference-sequence entries on the fused path: b3v and the c-step (cv + ch over the processing
+// order) with the production kernels' column-group shape
+hipError_t launch_b3v_cols(int n_owned, int nl, const int *nlev, const real *plus, const real *minus, real *adf_v,
+                           hipStream_t s);
+hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
 hipError_t launch_b3h_edges(const int4 *einfo, int count, int nl, const real *plus, const real *minus,

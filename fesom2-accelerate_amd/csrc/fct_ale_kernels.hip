@@ -732,6 +732,104 @@ __global__ __launch_bounds__(1024) void k_b3h_n(const NodeInfo *__restrict__ inf
     }
 }
 
+// ============================================================================ reference-sequence
+// entries on the fused path: fct_ale_inter_comm_acc_ (b3v) and fct_ale_c_acc_ (cv + ch) with the
+// column-group shape of the production kernels (the one-wave-per-column kernels above stay for the
+// stepwise path).
+
+// b3-vertical, G consecutive owned columns per block (index order), level pairs.
+template <int C, bool ODD>
+__global__ __launch_bounds__(1024) void k_b3v_g(int n_owned, int L, int G, float invS, const int *__restrict__ nlev,
+                                                const real *__restrict__ plus, const real *__restrict__ minus,
+                                                real *__restrict__ adf_v)
+{
+    int j, u;
+    slot_of(threadIdx.x, (L + C - 1) / C, invS, j, u);
+    const int n = block_tile() * G + j;
+    if (j >= G || n >= n_owned) return;
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    const int Ln = nlev[n] - 1;
+    const int top = Ln > 1 ? Ln : 1;  // the Fortran always limits nz = 1
+    const int na = min(C, top - z0);
+    if (na <= 0) return;
+    const size_t b = (size_t)n * L + z0, ab = (size_t)n * (L + 1) + z0;
+    real f[C], p[C], m[C];
+    ld_nl<C, true>(adf_v + ab, na, f, 0.);
+    ldo<C, ODD>(plus + b, p, last1);
+    ldo<C, ODD>(minus + b, m, last1);
+    const real pm = z0 ? plus[b - 1] : 0., mm = z0 ? minus[b - 1] : 0.;
+    real out[C];
+#pragma unroll
+    for (int c = 0; c < C; c++)
+        out[c] = b3v_factor(z0 + c, f[c], c ? p[c - 1] : pm, c ? m[c - 1] : mm, p[c], m[c]) * f[c];
+    if constexpr (C == 2) {
+        if (na == 2) {
+            f2a_d2u t;
+            t.x = out[0];
+            t.y = out[1];
+            *reinterpret_cast<f2a_d2u *>(adf_v + ab) = t;
+            return;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++)
+        if (c < na) adf_v[ab + c] = out[c];
+}
+
+// c-step (docs/refactoring.md:292-314): c-vertical and c-horizontal of the block's G columns in
+// processing order, one area load for both; the arithmetic of k_cv / k_p2h.
+template <int C, int KB, bool ODD>
+__global__ __launch_bounds__(1024) void k_c(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    static_assert(C == 2, "level pairs");
+    extern __shared__ real lds[];  // NodeRec[G]
+    const int L = a.nl - 1, S = (L + C - 1) / C;
+    const int first = block_tile() * G;
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
+    int j, u;
+    slot_of(threadIdx.x, S, invS, j, u);
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    if (j >= ncol) return;
+    const NodeInfo ni = recs[j].info;
+    const int nw = max(0, min(C, ni.Ln - z0));
+    if (nw <= 0) return;
+    const size_t b = (size_t)ni.n * L + z0, ab = (size_t)ni.n * a.nl + z0;
+    real dv[C], tt[C], hn[C], lo[C], hnn[C], dh[C], ar[C], v[C + 1], dta[C];
+    ldo<C, ODD>(a.del_v + b, dv, last1);
+    ldo<C, ODD>(a.ttf + b, tt, last1);
+    ldo<C, ODD>(a.hnode + b, hn, last1);
+    ldo<C, ODD>(a.LO + b, lo, last1);
+    ldo<C, ODD>(a.hnode_new + b, hnn, last1);
+    ldo<C, ODD>(a.del_h + b, dh, last1);
+    ld_nl<C, true>(a.area + ab, nw, ar, 1.);
+    {   // fct_adf_v at z0, z0+1 (a 16-byte load at 8-byte alignment, both inside the column: z0+1 <= L)
+        // and z0+2 when both levels are wet (z0+2 <= Ln <= L)
+        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(a.adf_v + ab);
+        v[0] = t.x;
+        v[1] = t.y;
+        v[2] = nw == 2 ? a.adf_v[ab + 2] : 0.;
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++) dta[c] = a.dt / ar[c];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        real t = dv[c] - tt[c] * hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
+        t = t + lo[c] * hnn[c];
+        dv[c] = t + (v[c] - v[c + 1]) * dta[c];
+    }
+    const int ne = ni.e1 - ni.e0;
+    auto add = [&](int c, real h, int second) {
+        dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+    };
+    for_edges<C, KB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+    if (ne > kRecEdge) for_edges<C, KB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
+    stv<C>(a.del_v + b, dv, nw);
+    stv<C>(a.del_h + b, dh, nw);
+}
+
 template <int C, int KB, bool NT>
 __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, float invS)
 {
@@ -1178,6 +1276,32 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_b3v_cols(int n_owned, int nl, const int *nlev, const real *plus, const real *minus, real *adf_v,
+                           hipStream_t s)
+{
+    const int L = nl - 1;
+    const bool odd = L % 2 == 1;
+    if (odd && L < 3) return launch_b3v(n_owned, nl, nlev, plus, minus, adf_v, s);
+    const int S = (L + 1) / 2, G = group_columns(S);
+    const long groups = (n_owned + G - 1) / G;
+    const float invS = 1.0f / (float)S;
+    if (odd) F2A_LAUNCH_GROUPS((k_b3v_g<2, true>), groups, G, S, 0, s, n_owned, L, G, invS, nlev, plus, minus, adf_v);
+    F2A_LAUNCH_GROUPS((k_b3v_g<2, false>), groups, G, S, 0, s, n_owned, L, G, invS, nlev, plus, minus, adf_v);
+}
+
+hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1;
+    const bool odd = L % 2 == 1;
+    if (odd && L < 3) return hipErrorInvalidValue;
+    const int S = (L + 1) / 2, G = group_columns(S);
+    const long groups = (a.count + G - 1) / G;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec);
+    if (odd) F2A_LAUNCH_GROUPS((k_c<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_c<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,

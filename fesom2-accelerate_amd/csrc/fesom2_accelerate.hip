@@ -359,7 +359,12 @@ void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **f
     Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v");
     Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
     if (!bplus || !bminus || !badfv || !bnl) return;
-    if (!run("fct_ale_b3_vertical", st, [&] { return f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st); }))
+    const bool stepwise = kernel_path() == 1;
+    if (!run("fct_ale_b3_vertical", st, [&] {
+            return stepwise ? f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st)
+                            : f2a::launch_b3v_cols(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus),
+                                                   dptr<real>(badfv), st);
+        }))
         return;
     *alg_state = 7;
     if (!g_resident && !d2h_async(badfv, st)) *alg_state = 0;
@@ -389,8 +394,15 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
     if (!plan) return;
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
-    if (!run("fct_ale_b3_horizontal", st, [&] { return f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus), dptr<real>(bminus),
-                            dptr<real>(badfh), st); }))
+    // fused path: the production edge kernel over the plan's edge list (edge index order here)
+    const bool stepwise = kernel_path() == 1;
+    if (!run("fct_ale_b3_horizontal", st, [&] {
+            if (!stepwise && plan->dev.p_edge_info)
+                return f2a::launch_b3h_fused(plan->dev, NL, 0, E, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
+                                             f2a::Tracers{}, st);
+            return f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus),
+                                   dptr<real>(bminus), dptr<real>(badfh), st);
+        }))
         return;
     *alg_state = 8;
     if (!g_resident && !d2h_async(badfh, st)) *alg_state = 0;
@@ -422,11 +434,20 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
     mh.nlev_nod = bnl;
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
-    if (!run("fct_ale_c_vertical", st, [&] { return f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
-                           dptr<real>(badfv), dptr<real>(barea), dptr<real>(bdv), *dt, st); }))
-        return;
-    if (!run("fct_ale_c_horizontal", st, [&] { return f2a::launch_ch(plan->dev, NL, dptr<real>(badfh), dptr<real>(barea), dptr<real>(bdh), *dt, st); }))
-        return;
+    const f2a::MeshPlanDev &d = plan->dev;
+    if (kernel_path() != 1 && d.p2_rec && (L % 2 == 0 || L >= 3)) {
+        // fused path: cv + ch in one node kernel over the processing order
+        f2a::P2Args a{NL, d.p2_rec, N, nullptr, nullptr, dptr<real>(bttf), dptr<real>(blo), dptr<real>(bh),
+                      dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh), dptr<real>(bdv),
+                      dptr<real>(bdh), *dt};
+        if (!run("fct_ale_c", st, [&] { return f2a::launch_c_fused(d, a, st); })) return;
+    } else {
+        if (!run("fct_ale_c_vertical", st, [&] { return f2a::launch_cv(N, NL, dptr<int>(bnl), dptr<real>(bttf), dptr<real>(bh), dptr<real>(blo), dptr<real>(bhn),
+                               dptr<real>(badfv), dptr<real>(barea), dptr<real>(bdv), *dt, st); }))
+            return;
+        if (!run("fct_ale_c_horizontal", st, [&] { return f2a::launch_ch(plan->dev, NL, dptr<real>(badfh), dptr<real>(barea), dptr<real>(bdh), *dt, st); }))
+            return;
+    }
     *alg_state = 9;
     if (!g_resident && (!d2h_async(bdv, st) || !d2h_async(bdh, st))) *alg_state = 0;
 }

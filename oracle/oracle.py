@@ -234,6 +234,21 @@ def ref_pre_comm(m, f, eps=1e-16, big=1e3, dt=1.0):
     return dict(ttf_max=tmax, ttf_min=tmin, plus=plus, minus=minus, UV=UV)
 
 
+def time_ref_pre_comm(m, f, reps=2):
+    """Best wall time of reference.cpp's CPU path (a1..a4 = a1..b2, the whole of what the reference
+    implements on the CPU), or None without _ref (bench.py's cpu_baseline, kind "reference")."""
+    import time
+    if ref() is None:
+        return None
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ref_pre_comm(m, f)
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    return best
+
+
 def b1h(nlev_elem, nl, n_edges, plus, minus, adf_h, edges, edge_tri):
     lib().oracle_b1h(_ptr(nlev_elem), _I(nl), _I(n_edges), _ptr(plus), _ptr(minus), _ptr(adf_h), _ptr(edges),
                      _ptr(edge_tri))

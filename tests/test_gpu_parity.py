@@ -412,17 +412,17 @@ def run_split(m, f):
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 6, 48, 81, 129, 200])
 @pytest.mark.parametrize("full", [False, True])
-@pytest.mark.parametrize("split", [False, True])
-def test_level_counts(nl, full, split):
+@pytest.mark.parametrize("mode", ["fused", "sequence", "split"])
+def test_level_counts(nl, full, mode):
     """Level counts from the minimum to deep columns, odd and even L (one or two levels per thread,
     odd L in pairs with a one-level last slot on the split path, columns per block from 1 to 64,
     80-level columns and 128/199-level ones)."""
     m = synth.make_mesh(40, 14, nl, full_depth=full)
     f = synth.make_fields(m)
-    if split:
+    if mode == "split":
         got = run_split(m, f)
-    else:
-        st, got = run_pass(m, f)
+    else:  # fused: pre_comm -> post_comm_c; sequence: pre_comm -> inter_comm -> post_comm -> c
+        st, got = run_pass(m, f, fused=mode == "fused")
         assert st == 9
     check_pass(m, got, O.full_pass(m, f))
 
