@@ -1170,8 +1170,18 @@ int fused_group_columns(int nl)
     return group_columns(L / levels_per_thread(L));
 }
 
+// odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0: one level
+// per thread)
+static bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && env_int("FESOM2_ODD_PAIR", 1) != 0; }
+
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
+    if (odd_pairs(a.nl - 1) && a.vlimit == 1 && !env_int("FESOM2_P1_EDGE", 0) && !env_int("FESOM2_P1_STAGE", 0)) {
+        const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, false, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
+    }
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     // opt-in phase-1 variants (fct_ale_variants.hip)
@@ -1187,10 +1197,6 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     default: return C == 2 ? p1_launch<2, 2, 2>(mp, a, s, G, S, groups) : p1_launch<1, 2, 2>(mp, a, s, G, S, groups);
     }
 }
-
-// odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0: one level
-// per thread)
-static bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && env_int("FESOM2_ODD_PAIR", 1) != 0; }
 
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
