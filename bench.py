@@ -30,6 +30,7 @@ for the multi-rank control plane (gloo: barrier, max-reduce, RCCL unique-id broa
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -235,6 +236,10 @@ def main():
                          "pre_comm -> inter_comm -> post_comm -> c with the fused phase 1")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
+    ap.add_argument("--transfers", action="store_true",
+                    help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
+                         "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
+                         "sequence; a PCIe-inclusive rate for DESIGN.md, not the benchmark value (1 GPU, 1 tracer)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
                          "oracle on the global mesh (gathered over ranks)")
@@ -285,7 +290,24 @@ def main():
         raise SystemExit("--tracers > 1 runs the batched (fused or split) entry points only")
     fields = synth.make_tracer_fields(m, args.tracers)
     f = fields[0]
-    abi.set_resident(True)
+    pinned = []
+    if args.transfers:
+        if world > 1 or args.tracers > 1 or args.check:
+            raise SystemExit("--transfers: 1 GPU, 1 tracer, no --check (outputs land in the input host arrays)")
+        args.path = "reference"
+        pf = {}
+        zeros = np.zeros((m.N + m.H) * m.L)
+        for k, v in list(f.items()) + [("plus", zeros), ("minus", zeros)]:
+            # page-locked host arrays, as FESOM2 would use allocate_pinned_doubles_
+            hp, st = C.c_void_p(), C.c_int(0)
+            abi.dll().allocate_pinned_doubles_(C.byref(hp), C.byref(C.c_int(v.size)), C.byref(st))
+            a = np.ctypeslib.as_array((C.c_double * v.size).from_address(hp.value))
+            a[:] = v
+            pf[k] = a
+            pinned.append(hp)
+        fields = [pf]
+        f = pf
+    abi.set_resident(not args.transfers)
     abi.set_path("stepwise" if args.path == "stepwise" else "fused")
     dm = engine.DeviceMesh(m)
     dm.prepare()
@@ -294,7 +316,6 @@ def main():
 
     halo = None
     if world > 1 and args.exchange == "rccl":
-        import ctypes as C
         uid = engine.Halo.unique_id() if rank == 0 else (C.c_char * 128)()
         t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
         dist.broadcast(t, src=0)
@@ -321,7 +342,23 @@ def main():
         e.upload("plus", pm[0].reshape(-1))
         e.upload("minus", pm[1].reshape(-1))
 
+    def step_transfers():
+        """FESOM2 with the reference's transfer semantics: the producer uploads ttf/adf_v/adf_h
+        (src/fesom2-accelerate.cu:269-270), each phase moves its own fields, the host waits after
+        phase 1 (where exchange_nod would run) and at the end."""
+        import ctypes as C
+        for k in ("ttf", "adf_v", "adf_h"):
+            abi.dll().transfer_var_async_(e.h[k].ref, abi.arr(e.host[k]), e.stream.ref, C.byref(C.c_bool(True)))
+        if e.pre_comm() != 6:
+            raise RuntimeError(f"pre_comm: {abi.last_error()}")
+        e.sync()
+        if (e.inter_comm(), e.post_comm(), e.c_step())[-1] != 9:
+            raise RuntimeError(f"phase 2: {abi.last_error()}")
+        e.sync()
+
     def step():
+        if args.transfers:
+            return step_transfers()
         if args.path == "split":
             s1 = e.pre_comm_v()
             if s1 != 7:
@@ -471,6 +508,8 @@ def main():
                               "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
             "kernels": per_kernel,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "transfers": "reference transfer semantics, PCIe inside the timed step" if args.transfers else
+                         "device resident (inputs in HBM before the timed region)",
             "setup_s": round(setup_s, 1),
         }
         if check is not None:
@@ -479,6 +518,8 @@ def main():
 
     e.free()
     dm.free()
+    for hp in pinned:
+        abi.dll().fesom2_free_pinned_(C.byref(hp))
     if halo is not None:
         halo.free()
     if dist is not None:
