@@ -108,9 +108,10 @@ __device__ __forceinline__ real b3h_factor(real flux, real p1, real m1, real p2,
 
 // ============================================================================ fused kernels
 //
-// C levels per thread (C = 2 when L is even: ttf/LO/adf_h/plus/minus/del_* are then read and written
-// as 16-byte pairs; arrays of stride nl = L+1 -- fct_adf_v, area, area_inv -- stay 8-byte because
-// their columns alternate 16-byte alignment).  A block owns G whole columns (node columns for phases
+// C levels per thread (C = 2: ttf/LO/adf_h/plus/minus/del_* are read and written as 16-byte pairs;
+// the stride-nl arrays -- fct_adf_v, area, area_inv -- and odd-L columns start at 8-byte alignment,
+// which a 16-byte access tolerates on gfx950 (f2a_d2u below); for odd L the last slot of a column
+// holds one level, see ldo).  A block owns G whole columns (node columns for phases
 // 1/2, edge columns for b3h) taken in the plan's processing order; thread t is the level pair
 // z0 = C*(t % (L/C)) of column t / (L/C), and the block has G*L/C threads rounded up to the wave
 // size (L = 80, C = 2, G = 8: 320 threads, 5 full waves).  A column group completes within one chain
