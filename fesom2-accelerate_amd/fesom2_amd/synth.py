@@ -110,6 +110,50 @@ def make_mesh(nx, ny, nl, seed=42, full_depth=False, name=""):
                 edge_gid=np.arange(E, dtype=np.int64), name=name or f"{nx}x{ny}x{nl - 1}")
 
 
+def delaunay_mesh(npts, nl, seed=11, full_depth=False, name=""):
+    """Unstructured variant: the Delaunay triangulation of ``npts`` random points in the unit square.
+
+    Node degrees vary (3 .. ~12, unlike the structured mesh's 6), so clusters and edge lists overflow
+    the 8 inline NodeRec entries; the numbering is scipy's (scattered).  Same array conventions as
+    :func:`make_mesh` (1-based, ``edge_tri`` second entry 0 on the boundary, element levels uniform in
+    [3, nl] unless ``full_depth``, node levels = max over the adjacent elements).
+    """
+    from scipy.spatial import Delaunay
+
+    rng = np.random.default_rng(seed)
+    tri = Delaunay(rng.random((npts, 2))).simplices.astype(np.int64)  # (T, 3), 0-based
+    T = len(tri)
+    e = np.concatenate([tri[:, [0, 1]], tri[:, [1, 2]], tri[:, [2, 0]]])
+    e.sort(axis=1)
+    uniq, inv = np.unique(e[:, 0] * npts + e[:, 1], return_inverse=True)
+    E = len(uniq)
+    edges = np.stack([uniq // npts, uniq % npts], axis=1)
+    tri_of = np.tile(np.arange(T), 3)
+    order = np.argsort(inv, kind="stable")
+    cnt = np.bincount(inv, minlength=E)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    et = np.zeros((E, 2), np.int64)
+    et[:, 0] = tri_of[order[start]] + 1
+    two = cnt == 2
+    et[two, 1] = tri_of[order[start[two] + 1]] + 1
+    # nod_in_elem2D: the elements around each node, padded with 0
+    flat = tri.reshape(-1)
+    deg = np.bincount(flat, minlength=npts)
+    dim = int(deg.max())
+    o = np.argsort(flat, kind="stable")
+    pos = np.arange(flat.size) - np.concatenate([[0], np.cumsum(deg)[:-1]])[flat[o]]
+    nie = np.zeros((npts, dim), np.int64)
+    nie[flat[o], pos] = o // 3 + 1
+    le = np.full(T, nl, np.int64) if full_depth else rng.integers(3, nl + 1, T)
+    ln = np.zeros(npts, np.int64)
+    np.maximum.at(ln, tri.reshape(-1), np.repeat(le, 3))
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32).reshape(-1)
+    return Mesh(nl=nl, N=npts, H=0, T=T, E=E, dim=dim, elem2D_nodes=i32(tri + 1), edges=i32(edges + 1),
+                edge_tri=i32(et), nie_num=i32(deg), nie=i32(nie), nlev_elem=i32(le), nlev_nod=i32(ln),
+                node_gid=np.arange(npts, dtype=np.int64), edge_gid=np.arange(E, dtype=np.int64),
+                name=name or f"delaunay{npts}x{nl - 1}")
+
+
 def config_mesh(name, full_depth=False, seed=42):
     nx, ny, nl = CONFIGS[name]
     return make_mesh(nx, ny, nl, seed=seed, full_depth=full_depth, name=name)

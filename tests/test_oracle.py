@@ -73,6 +73,20 @@ def test_oracle_matches_reference_cpp(name, full, perm):
         assert np.array_equal(got[k].view(np.uint64), want[k].view(np.uint64)), k
 
 
+@pytest.mark.skipif(O.ref() is None, reason="oracle/_ref (reference.cpp build) not present")
+@pytest.mark.parametrize("npts,nl,full", [(3000, 21, False), (2000, 48, True), (5000, 12, False)])
+def test_oracle_matches_reference_cpp_unstructured(npts, nl, full):
+    """Delaunay meshes: node degrees 3..13 and scattered numbering (the structured meshes have 6)."""
+    m = synth.delaunay_mesh(npts, nl, full_depth=full)
+    assert m.dim > 8
+    f = synth.make_fields(m)
+    st, got = O.pre_comm(m, f)
+    assert st == 5
+    want = O.ref_pre_comm(m, f)
+    for k in ("ttf_max", "ttf_min", "plus", "minus", "UV"):
+        assert np.array_equal(got[k].view(np.uint64), want[k].view(np.uint64)), k
+
+
 def test_vlimit_protocol_of_reference_cpp():
     """reference.cpp runs a3/a4 only for vlimit == 1 and reports alg_state 2 otherwise (:297-303)."""
     m = synth.config_mesh("tiny")
