@@ -274,6 +274,37 @@ namespace f2a {
 
 // ----------------------------------------------------------------------------- plans
 
+// Packed b3h blocks (MeshPlanDev::b3p_*): greedy over the edge list, separately for [0, n_int) and
+// [n_int, E) so the exchange-overlap split keeps working.
+static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_int)
+{
+    std::vector<int2> desc;
+    std::vector<unsigned short> off(einfo.size());
+    int nint = 0;
+    for (int part = 0; part < 2; part++) {
+        const int k_end = part ? (int)einfo.size() : n_int;
+        int k = part ? n_int : 0;
+        while (k < k_end) {
+            const int k0 = k;
+            int slots = 0;
+            while (k < k_end && k - k0 < kB3hPackEdges) {
+                const int s = (einfo[k].z + 1) / 2;
+                if (slots + s > kB3hPackSlots) break;
+                off[k] = (unsigned short)slots;
+                slots += s;
+                k++;
+            }
+            desc.push_back(make_int2(k0, k - k0));
+        }
+        if (!part) nint = (int)desc.size();
+    }
+    d.b3p_desc = plan->mem.upload(desc);
+    d.b3p_off = plan->mem.upload(off);
+    d.b3p_nint = nint;
+    d.b3p_ndesc = (int)desc.size();
+    return desc.empty() || (d.b3p_desc && d.b3p_off);
+}
+
 std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
                                  int n_csr, int nl, std::string &err)
 {
@@ -707,7 +738,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         d.p_edges = plan->mem.upload(pedges);
         d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.node_info || !d.node_rec || !d.p2_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info)
+        if (!d.node_info || !d.node_rec || !d.p2_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info ||
+            !build_b3h_pack(plan.get(), d, einfo, d.n_edge_interior))
             return fail("device allocation for the processing order failed");
     } else if (n_edges > 0) {
         std::vector<int4> einfo(n_edges);
@@ -715,7 +747,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             einfo[e] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
         d.n_edge_interior = n_edges;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.p_edge_info) return fail("device allocation for the edge list failed");
+        if (!d.p_edge_info || !build_b3h_pack(plan.get(), d, einfo, n_edges))
+            return fail("device allocation for the edge list failed");
     }
     return plan;
 }

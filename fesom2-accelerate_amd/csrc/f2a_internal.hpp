@@ -59,6 +59,7 @@ struct NodeInfo {
 // depend on a single global load instead of NodeInfo -> CSR -> gather.  Entries beyond the inline
 // capacity stay in the processing-order CSRs at [r0 + kRecRing, r1) / [e0 + kRecEdge, e1).
 constexpr int kRecRing = 8, kRecEdge = 8;
+constexpr int kB3hPackSlots = 640, kB3hPackEdges = 256;  // packed b3h block: level pairs, edges
 struct alignas(16) NodeRec {
     NodeInfo info;
     RingRef ring[kRecRing];
@@ -89,6 +90,12 @@ struct MeshPlanDev {
     const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order,
                                           // interior edges (both endpoints owned) first
     int n_edge_interior = 0;
+    // packed b3h (variable depth): blocks of consecutive p_edge_info edges holding at most
+    // kB3hPackSlots level pairs; b3p_desc[b] = {first edge, edges}, b3p_off[k] = slot offset of edge k
+    // in its block; descriptors [0, b3p_nint) cover the interior edges, the rest the boundary ones
+    const int2 *b3p_desc = nullptr;
+    const unsigned short *b3p_off = nullptr;
+    int b3p_nint = 0, b3p_ndesc = 0;
     const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
     const int *p_owner_cum = nullptr;     // [n_owned + 1]: edges owned by processing positions < k
     // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of

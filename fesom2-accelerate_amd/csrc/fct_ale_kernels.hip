@@ -662,6 +662,72 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 }
 
 
+// b3-horizontal packed by depth: a block takes the consecutive edges of its descriptor, each with
+// ceil(lev/2) level-pair slots (not L/2: shallow edges leave no idle slots), at most kB3hPackSlots
+// slots, two per thread (both slots' loads in flight together, as k_b3h_u's two groups).  The
+// block's edge infos and slot offsets go to LDS; a thread finds its edge by binary search.
+template <bool NT, bool ODD>
+__global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, const unsigned short *__restrict__ off,
+                                                const int4 *__restrict__ einfo, int L, const real *__restrict__ plus,
+                                                const real *__restrict__ minus, real *__restrict__ adf_h, Tracers trs)
+{
+    __shared__ int4 s_ei[kB3hPackEdges];
+    __shared__ int s_off[kB3hPackEdges + 1];
+    int tr;
+    const int g = group_tracer(trs.n, tr, c_tracer_major & 2);
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
+    const int2 dsc = desc[g];
+    const int t = threadIdx.x, n = dsc.y;
+    for (int i = t; i < n; i += blockDim.x) {
+        const int4 ei = einfo[dsc.x + i];
+        s_ei[i] = ei;
+        s_off[i] = off[dsc.x + i];
+        if (i == n - 1) s_off[n] = off[dsc.x + i] + (ei.z + 1) / 2;
+    }
+    __syncthreads();
+    constexpr int C = 2;
+    int q[2], z0[2];
+    bool act[2];
+    real f[2][C], p1[2][C], m1[2][C], p2[2][C], m2[2][C];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int slot = t + h * (int)blockDim.x;
+        act[h] = n > 0 && slot < s_off[n];
+        int lo = 0, hi = n - 1;  // last edge with s_off <= slot
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= slot) lo = mid;
+            else hi = mid - 1;
+        }
+        q[h] = lo;
+        z0[h] = act[h] ? C * (slot - s_off[lo]) : 0;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if (!act[h]) continue;
+        const int4 ei = s_ei[q[h]];
+        const bool last1 = ODD && z0[h] + 1 == L;
+        ldo_s<C, NT, ODD>(adf_h + (size_t)ei.w * L + z0[h], f[h], last1);
+        const size_t i1 = (size_t)ei.x * L + z0[h], i2 = (size_t)ei.y * L + z0[h];
+        ldo<C, ODD>(plus + i1, p1[h], last1);
+        ldo<C, ODD>(minus + i1, m1[h], last1);
+        ldo<C, ODD>(plus + i2, p2[h], last1);
+        ldo<C, ODD>(minus + i2, m2[h], last1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if (!act[h]) continue;
+        const int4 ei = s_ei[q[h]];
+        const int nw = min(C, ei.z - z0[h]);
+        real out[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) out[c] = b3h_factor(f[h][c], p1[h][c], m1[h][c], p2[h][c], m2[h][c]) * f[h][c];
+        stv_s<C, NT>(adf_h + (size_t)ei.w * L + z0[h], out, nw);
+    }
+}
+
 template <int C, int U, bool NT, bool ODD = false>
 __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, int n_edges, int L,
                                                 int G, float invS, const real *__restrict__ plus,
@@ -1345,6 +1411,32 @@ hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int 
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
+    // packed by depth (FESOM2_B3H_PACK=1): the plan's descriptors for exactly these edge ranges
+    const int L = nl - 1;
+    if (mp.b3p_desc && env_int("FESOM2_B3H_PACK", 1) && (L % 2 == 0 || odd_pairs(L))) {
+        int d0 = -1, d1 = -1;
+        if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc;
+        else if (begin == 0 && count == mp.n_edge_interior) d0 = 0, d1 = mp.b3p_nint;
+        else if (begin == mp.n_edge_interior && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc;
+        if (d0 >= 0) {
+            const long groups = (long)(d1 - d0) * tr.n;
+            const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
+            init_swizzle();
+            if (groups <= 0) return hipSuccess;
+            const dim3 grid((unsigned)groups), block(kB3hPackSlots / 2);
+            if (L % 2) {
+                hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off, mp.p_edge_info,
+                                   L, plus, minus, adf_h, tr);
+            } else if (NT) {
+                hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
+                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
+            } else {
+                hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
+                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
+            }
+            return hipGetLastError();
+        }
+    }
     return launch_b3h_edges(mp.p_edge_info + begin, count, nl, plus, minus, adf_h, tr, s);
 }
 

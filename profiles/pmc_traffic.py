@@ -20,7 +20,8 @@ import json
 import sys
 
 NAMES = {"k_p1": "fct_ale_p1", "k_p1v": "fct_ale_p1v", "k_p2": "fct_ale_p2", "k_p2h": "fct_ale_p2h",
-         "k_b3h_g": "fct_ale_b3_horizontal", "k_b3h_u": "fct_ale_b3_horizontal", "k_p2f": "fct_ale_p2_b3h"}
+         "k_b3h_g": "fct_ale_b3_horizontal", "k_b3h_u": "fct_ale_b3_horizontal",
+         "k_b3h_p": "fct_ale_b3_horizontal", "k_p2f": "fct_ale_p2_b3h"}
 
 
 def kernel_key(name):

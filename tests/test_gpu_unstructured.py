@@ -53,6 +53,14 @@ def test_unstructured_paths_match_oracle(npts, nl, full, mode):
     check_pass(m, got, O.full_pass(m, f))
 
 
+@pytest.mark.parametrize("npts,nl,full", MESHES)
+def test_unstructured_packed_b3h(npts, nl, full, monkeypatch):
+    """b3h packed by depth (FESOM2_B3H_PACK=1) on variable-depth unstructured meshes."""
+    monkeypatch.setenv("FESOM2_B3H_PACK", "1")
+    m, f = mesh(npts, nl, full)
+    check_pass(m, run_split(m, f), O.full_pass(m, f))
+
+
 @pytest.mark.parametrize("npts,nl,full", MESHES[:2])
 def test_unstructured_batched_split(npts, nl, full):
     m, _ = mesh(npts, nl, full)
