@@ -666,7 +666,7 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 // ceil(lev/2) level-pair slots (not L/2: shallow edges leave no idle slots), at most kB3hPackSlots
 // slots, two per thread (both slots' loads in flight together, as k_b3h_u's two groups).  The
 // block's edge infos and slot offsets go to LDS; a thread finds its edge by binary search.
-template <bool NT, bool ODD>
+template <bool NT, bool ODD, int H = 2>
 __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, const unsigned short *__restrict__ off,
                                                 const int4 *__restrict__ einfo, int L, const real *__restrict__ plus,
                                                 const real *__restrict__ minus, real *__restrict__ adf_h, Tracers trs)
@@ -688,11 +688,11 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
     }
     __syncthreads();
     constexpr int C = 2;
-    int q[2], z0[2];
-    bool act[2];
-    real f[2][C], p1[2][C], m1[2][C], p2[2][C], m2[2][C];
+    int q[H], z0[H];
+    bool act[H];
+    real f[H][C], p1[H][C], m1[H][C], p2[H][C], m2[H][C];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < H; h++) {
         const int slot = t + h * (int)blockDim.x;
         act[h] = n > 0 && slot < s_off[n];
         int lo = 0, hi = n - 1;  // last edge with s_off <= slot
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
         z0[h] = act[h] ? C * (slot - s_off[lo]) : 0;
     }
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < H; h++) {
         if (!act[h]) continue;
         const int4 ei = s_ei[q[h]];
         const bool last1 = ODD && z0[h] + 1 == L;
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
         ldo<C, ODD>(minus + i2, m2[h], last1);
     }
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < H; h++) {
         if (!act[h]) continue;
         const int4 ei = s_ei[q[h]];
         const int nw = min(C, ei.z - z0[h]);
@@ -1423,7 +1423,18 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
             const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
             init_swizzle();
             if (groups <= 0) return hipSuccess;
-            const dim3 grid((unsigned)groups), block(kB3hPackSlots / 2);
+            const int H = env_int("FESOM2_B3HP_H", 2);
+            const dim3 grid((unsigned)groups), block(kB3hPackSlots / H);
+            if (H == 1 && !(L % 2) && NT) {
+                hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
+                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
+                return hipGetLastError();
+            }
+            if (H == 4 && !(L % 2) && NT) {
+                hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
+                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
+                return hipGetLastError();
+            }
             if (L % 2) {
                 hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off, mp.p_edge_info,
                                    L, plus, minus, adf_h, tr);
