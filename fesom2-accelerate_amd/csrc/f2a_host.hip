@@ -281,6 +281,8 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     std::vector<int2> desc;
     std::vector<unsigned short> off(einfo.size());
     int nint = 0;
+    const char *cenv = getenv("FESOM2_B3HP_CAP");  // level pairs per block (A/B; default kB3hPackSlots)
+    const int cap = std::max(64, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048));
     for (int part = 0; part < 2; part++) {
         const int k_end = part ? (int)einfo.size() : n_int;
         int k = part ? n_int : 0;
@@ -289,7 +291,7 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
             int slots = 0;
             while (k < k_end && k - k0 < kB3hPackEdges) {
                 const int s = (einfo[k].z + 1) / 2;
-                if (slots + s > kB3hPackSlots) break;
+                if (slots + s > cap) break;
                 off[k] = (unsigned short)slots;
                 slots += s;
                 k++;
@@ -301,6 +303,7 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     d.b3p_desc = plan->mem.upload(desc);
     d.b3p_off = plan->mem.upload(off);
     d.b3p_nint = nint;
+    d.b3p_cap = cap;
     d.b3p_ndesc = (int)desc.size();
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }

@@ -95,7 +95,7 @@ struct MeshPlanDev {
     // in its block; descriptors [0, b3p_nint) cover the interior edges, the rest the boundary ones
     const int2 *b3p_desc = nullptr;
     const unsigned short *b3p_off = nullptr;
-    int b3p_nint = 0, b3p_ndesc = 0;
+    int b3p_nint = 0, b3p_ndesc = 0, b3p_cap = 0;  // b3p_cap: level pairs per block
     const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
     const int *p_owner_cum = nullptr;     // [n_owned + 1]: edges owned by processing positions < k
     // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of

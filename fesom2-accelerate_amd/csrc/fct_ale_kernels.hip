@@ -1424,7 +1424,7 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
             init_swizzle();
             if (groups <= 0) return hipSuccess;
             const int H = env_int("FESOM2_B3HP_H", 2);
-            const dim3 grid((unsigned)groups), block(kB3hPackSlots / H);
+            const dim3 grid((unsigned)groups), block((mp.b3p_cap + H - 1) / H);
             if (H == 1 && !(L % 2) && NT) {
                 hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
                                    mp.p_edge_info, L, plus, minus, adf_h, tr);

@@ -433,7 +433,8 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_PATCH_ORDER": "0", "FESOM2_PATCH": "64"}, {"FESOM2_B3H_NODE": "1"},
                {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "1"}, {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "3"},
                {"FESOM2_B3H_NODE": "1", "FESOM2_ODD_PAIR": "0"}, {"FESOM2_B3H_PACK": "0"},
-               {"FESOM2_B3H_PACK": "1", "FESOM2_B3H_NT": "0"}]
+               {"FESOM2_B3H_PACK": "1", "FESOM2_B3H_NT": "0"},
+               {"FESOM2_B3HP_H": "1"}, {"FESOM2_B3HP_H": "4"}, {"FESOM2_B3HP_CAP": "100"}]
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
