@@ -244,6 +244,9 @@ def main():
                          "pre_comm -> inter_comm -> post_comm -> c with the fused phase 1")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one step into a hipGraph after the warmup and time K replays (no host-side "
+                         "work per step; per-kernel timing and roofline are then not available)")
     ap.add_argument("--transfers", action="store_true",
                     help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
                          "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
@@ -405,8 +408,21 @@ def main():
     abi.device_sync()
     setup_s = time.perf_counter() - t_setup
 
+    graph = None
+    if args.graph:
+        if args.transfers or (world > 1 and args.exchange == "host"):
+            raise SystemExit("--graph needs device-resident steps without host exchange")
+        abi.device_sync()
+        with abi.Graph.capture(stream) as graph:
+            step()
+
+        def step():  # noqa: F811 -- the replay replaces the eager step in the timed region
+            graph.launch(stream)
+        step()
+        abi.device_sync()
+
     # ---- timed region: exactly K steps, barrier + device sync on both sides
-    abi.kernel_timing(True)
+    abi.kernel_timing(not args.graph)
     abi.kernel_timing_reset()
     barrier()
     abi.device_sync()
@@ -488,7 +504,9 @@ def main():
 
     check = None
     if args.check:
-        check = verify(args, e, step, m, fields, rank, world, dist)
+        check = verify(args, e, step, m, fields, rank, world, dist)  # a replay when --graph
+    if graph is not None:
+        graph.free()
 
     if rank == 0:
         out = {
@@ -517,6 +535,7 @@ def main():
                               "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
             "kernels": per_kernel,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "graph": bool(args.graph),
             "transfers": "reference transfer semantics, PCIe inside the timed step" if args.transfers else
                          "device resident (inputs in HBM before the timed region)",
             "setup_s": round(setup_s, 1),

@@ -4,6 +4,7 @@
 #include "f2a_host.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -146,9 +147,12 @@ bool d2h_async(Buffer *b, hipStream_t s)
     return ok(hipMemcpyAsync(b->host_pointer, b->device_pointer, b->size, hipMemcpyDeviceToHost, s), "D2H async");
 }
 
+// Inside a graph capture the buffer events (recorded outside it by transfer_var_async_) are not
+// waited on -- a captured stream may not wait on an event from outside the capture; the caller
+// orders the producers' uploads before the graph launch.
 void wait_event(Buffer *b, hipStream_t s)
 {
-    if (b->has_event) (void)hipStreamWaitEvent(s, b->event, 0);
+    if (b->has_event && !capturing()) (void)hipStreamWaitEvent(s, b->event, 0);
 }
 
 bool check_levels(int nl, const char *who)
@@ -207,6 +211,10 @@ void resolve_pending()
 }  // namespace
 
 bool timing_enabled() { return g_timing; }
+
+static std::atomic<bool> g_capturing{false};
+bool capturing() { return g_capturing.load(); }
+void set_capturing(bool on) { g_capturing.store(on); }
 
 void timing_begin(const char *name, hipStream_t s, void **token)
 {
@@ -779,6 +787,11 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                 n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0};
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.get();
+    if (capturing()) {  // building a plan copies host <-> device: not inside a graph capture
+        report("a mesh plan would be built during a graph capture: run the sequence once (or "
+               "fesom2_prepare_mesh_) before fesom2_graph_begin_");
+        return nullptr;
+    }
     if (h.edges->size < 2 * sizeof(int) * (size_t)n_edges || h.edge_tri->size < 2 * sizeof(int) * (size_t)n_edges) {
         report("edge handles hold fewer than myDim_edge2D = %d edges", n_edges);
         return nullptr;

@@ -52,6 +52,9 @@ bool check_levels(int nl, const char *who);
 // ---- per-kernel timing (fesom2_kernel_timing_): HIP events recorded around each launch on the
 //      launch stream while enabled; resolved when the statistics are read.
 bool timing_enabled();
+// a pass is being captured into a hipGraph (fesom2_graph_begin_): no timing events, no plan builds
+bool capturing();
+void set_capturing(bool on);
 void timing_begin(const char *name, hipStream_t s, void **token);
 void timing_end(void *token, hipStream_t s);
 // Launch through `f` with optional timing; reports failures under `name`.
@@ -59,7 +62,7 @@ template <class F>
 bool run(const char *name, hipStream_t s, F &&f)
 {
     void *tok = nullptr;
-    if (timing_enabled()) timing_begin(name, s, &tok);
+    if (timing_enabled() && !capturing()) timing_begin(name, s, &tok);
     const bool good = ok(f(), name);
     if (tok) timing_end(tok, s);
     return good;

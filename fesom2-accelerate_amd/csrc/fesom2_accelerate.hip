@@ -907,6 +907,73 @@ void fesom2_free_pinned_(void **hostptr)
 
 void fesom2_device_sync_(int *istat) { *istat = ok(hipDeviceSynchronize(), "hipDeviceSynchronize") ? 0 : 1; }
 
+// ---- hipGraph capture of a call sequence (device-resident mode).  Everything the entry points
+// enqueue on *s between begin and end -- kernels, the exchange's fork/join onto the halo stream and
+// its RCCL send/recv -- becomes one graph; launching it replays the sequence without the host-side
+// validation, plan lookups and per-kernel launches.  The meshes' plans must exist already (one
+// ordinary pass, or fesom2_prepare_mesh_).  Kernel timing is off while capturing.
+struct GraphHandle {
+    static constexpr uint32_t kMagic = 0xF2A6A9F1u;
+    uint32_t magic = kMagic;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+void fesom2_graph_begin_(int *istat, void **s)
+{
+    *istat = 1;
+    if (!g_resident) {
+        report("fesom2_graph_begin_: graph capture needs device-resident mode (fesom2_set_resident_(1))");
+        return;
+    }
+    const hipStream_t st = stream_of(s);
+    if (!st) {
+        report("fesom2_graph_begin_: the null stream cannot be captured");
+        return;
+    }
+    if (!ok(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture")) return;
+    f2a::set_capturing(true);
+    *istat = 0;
+}
+
+void fesom2_graph_end_(int *istat, void **s, void **graph)
+{
+    *istat = 1;
+    *graph = nullptr;
+    f2a::set_capturing(false);
+    auto *g = new GraphHandle;
+    if (!ok(hipStreamEndCapture(stream_of(s), &g->graph), "hipStreamEndCapture") ||
+        !ok(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0), "hipGraphInstantiate")) {
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return;
+    }
+    *graph = g;
+    *istat = 0;
+}
+
+void fesom2_graph_launch_(int *istat, void **graph, void **s)
+{
+    *istat = 1;
+    auto *g = graph && *graph ? static_cast<GraphHandle *>(*graph) : nullptr;
+    if (!g || g->magic != GraphHandle::kMagic) {
+        report("fesom2_graph_launch_: invalid graph handle");
+        return;
+    }
+    if (ok(hipGraphLaunch(g->exec, stream_of(s)), "hipGraphLaunch")) *istat = 0;
+}
+
+void fesom2_graph_free_(void **graph)
+{
+    auto *g = graph && *graph ? static_cast<GraphHandle *>(*graph) : nullptr;
+    if (!g || g->magic != GraphHandle::kMagic) return;
+    (void)hipGraphExecDestroy(g->exec);
+    (void)hipGraphDestroy(g->graph);
+    g->magic = 0;
+    delete g;
+    *graph = nullptr;
+}
+
 const char *fesom2_last_error(void) { return last_error(); }
 
 void fesom2_event_create_(void **ev, int *istat)

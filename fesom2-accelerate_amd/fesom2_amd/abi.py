@@ -31,6 +31,7 @@ EXPORTS = (
     "fct_ale_exchange_post_comm_c_batched_acc_", "fct_ale_post_comm_iter_acc_",
     "fct_ale_post_comm_iter_batched_acc_", "fesom2_exchange_nod_acc_",
     "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_", "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_",
+    "fesom2_graph_begin_", "fesom2_graph_end_", "fesom2_graph_launch_", "fesom2_graph_free_",
 )
 
 _dll = None
@@ -152,6 +153,45 @@ class Event(Handle):
     def free(self):
         if self:
             dll().fesom2_event_free_(self.ref)
+
+
+class Graph(Handle):
+    """hipGraph of a captured call sequence: ``with Graph.capture(stream) as g: <entry calls>``,
+    then ``g.launch(stream)`` replays it (device-resident mode, plans built beforehand)."""
+
+    def __init__(self):
+        super().__init__("graph")
+
+    @classmethod
+    def capture(cls, stream):
+        return _Capture(cls(), stream)
+
+    def launch(self, stream):
+        st = C.c_int(0)
+        dll().fesom2_graph_launch_(C.byref(st), self.ref, stream.ref)
+        check(st, "fesom2_graph_launch_")
+
+    def free(self):
+        if self:
+            dll().fesom2_graph_free_(self.ref)
+
+
+class _Capture:
+    def __init__(self, graph, stream):
+        self.graph, self.stream = graph, stream
+
+    def __enter__(self):
+        st = C.c_int(0)
+        dll().fesom2_graph_begin_(C.byref(st), self.stream.ref)
+        check(st, "fesom2_graph_begin_")
+        return self.graph
+
+    def __exit__(self, exc_type, exc, tb):
+        st = C.c_int(0)
+        dll().fesom2_graph_end_(C.byref(st), self.stream.ref, self.graph.ref)
+        if exc_type is None:
+            check(st, "fesom2_graph_end_")
+        return False
 
 
 def set_resident(on):

@@ -15,6 +15,7 @@
 ! mode 0: the reference sequence with the reference's transfer semantics (pre_comm -> inter_comm ->
 !         post_comm -> c; results land in the bound host arrays)
 ! mode 1: device resident, direction-split pass (pre_comm_v -> post_comm_h), results downloaded
+! mode 2: as 1, the pass captured into a hipGraph (fesom2_graph_*) after one eager pass, replayed
 ! OUT: int32(4) alg_states, then fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert,
 !      del_ttf_advhoriz in the IN format.
 program fct_ale_host
@@ -28,7 +29,7 @@ program fct_ale_host
                                          hnode_new(:), del_v(:), del_h(:), plus(:), minus(:), sc(:)
   type(c_ptr) :: s, h_nlev_nod, h_nlev_elem, h_elem_nodes, h_nie_num, h_nie, h_edges, h_edge_tri
   type(c_ptr) :: h_ttf, h_lo, h_adf_v, h_adf_h, h_area, h_area_inv, h_hnode, h_hnode_new, h_del_v, h_del_h, &
-                 h_plus, h_minus, h_tmax, h_tmin, h_uv, nullh
+                 h_plus, h_minus, h_tmax, h_tmin, h_uv, nullh, graph
   character(len=1024) :: fin, fout
   integer :: u
   logical(c_bool) :: yes, no
@@ -53,7 +54,7 @@ program fct_ale_host
   call set_mpi_rank(zero, one)
   call make_stream(s, istat)
   call check(istat, "make_stream")
-  if (mode == 1) call fesom2_set_resident(one)
+  if (mode >= 1) call fesom2_set_resident(one)
   ! mesh: once per run (reference .cu:114-127)
   call upload_mesh(h_nlev_nod, nlev_nod); call upload_mesh(h_nlev_elem, nlev_elem)
   call upload_mesh(h_elem_nodes, elem_nodes); call upload_mesh(h_nie_num, nie_num)
@@ -84,17 +85,27 @@ program fct_ale_host
     call await_stream(s, istat)
     call check(istat, "await_stream")
   else
-    call fct_ale_pre_comm_v_acc(st(1), s, ntr, h_plus, h_minus, h_ttf, h_lo, h_adf_v, h_adf_h, h_area_inv, h_area, &
-        h_hnode, h_hnode_new, h_del_v, N, H, T, E, nl, h_nlev_nod, h_nlev_elem, h_elem_nodes, h_nie_num, h_nie, &
-        dim, h_edges, h_edge_tri, vlimit, sc(2), sc(3), sc(1))
-    call fct_ale_post_comm_h_acc(st(2), s, ntr, nullh, nullh, h_plus, h_minus, h_adf_h, h_del_h, h_area, &
-        N, H, E, nl, h_nlev_nod, h_nlev_elem, h_edges, h_edge_tri, sc(1))
+    if (mode == 2) then
+      ! one eager pass builds the mesh plans, the pristine inputs go back up, and the pass is
+      ! captured into a hipGraph that the replay below runs instead of the entry calls
+      call split_pass()
+      call await_stream(s, istat)
+      call transfer_var(h_adf_v, adf_v); call transfer_var(h_adf_h, adf_h)
+      call transfer_var(h_del_v, del_v); call transfer_var(h_del_h, del_h)
+      call fesom2_graph_begin(istat, s); call check(istat, "fesom2_graph_begin")
+      call split_pass()
+      call fesom2_graph_end(istat, s, graph); call check(istat, "fesom2_graph_end")
+      call fesom2_graph_launch(istat, graph, s); call check(istat, "fesom2_graph_launch")
+    else
+      call split_pass()
+    end if
     call await_stream(s, istat)
     call check(istat, "await_stream")
     call fesom2_download(h_plus, plus, istat); call fesom2_download(h_minus, minus, istat)
     call fesom2_download(h_adf_v, adf_v, istat); call fesom2_download(h_adf_h, adf_h, istat)
     call fesom2_download(h_del_v, del_v, istat); call fesom2_download(h_del_h, del_h, istat)
     call check(istat, "fesom2_download")
+    if (mode == 2) call fesom2_graph_free(graph)
   end if
 
   open(newunit=u, file=trim(fout), access='stream', form='unformatted', status='replace')
@@ -105,6 +116,15 @@ program fct_ale_host
   print '(a, 4i3)', 'fct_ale_host: alg_state', st
 
 contains
+
+  ! the direction-split pass, device resident (fct_ale_pre_comm_v_acc_ -> fct_ale_post_comm_h_acc_)
+  subroutine split_pass()
+    call fct_ale_pre_comm_v_acc(st(1), s, ntr, h_plus, h_minus, h_ttf, h_lo, h_adf_v, h_adf_h, h_area_inv, h_area, &
+        h_hnode, h_hnode_new, h_del_v, N, H, T, E, nl, h_nlev_nod, h_nlev_elem, h_elem_nodes, h_nie_num, h_nie, &
+        dim, h_edges, h_edge_tri, vlimit, sc(2), sc(3), sc(1))
+    call fct_ale_post_comm_h_acc(st(2), s, ntr, nullh, nullh, h_plus, h_minus, h_adf_h, h_del_h, h_area, &
+        N, H, E, nl, h_nlev_nod, h_nlev_elem, h_edges, h_edge_tri, sc(1))
+  end subroutine
 
   subroutine check(istat, what)
     integer(c_int), intent(in) :: istat

@@ -126,5 +126,25 @@ module fesom2_accelerate
       import :: c_ptr
       type(c_ptr) :: stream
     end subroutine
+    ! ---- additions: hipGraph capture / replay of a call sequence (device-resident mode)
+    subroutine fesom2_graph_begin(istat, s) bind(C, name="fesom2_graph_begin_")
+      import :: c_ptr, c_int
+      integer(c_int) :: istat
+      type(c_ptr) :: s
+    end subroutine
+    subroutine fesom2_graph_end(istat, s, graph) bind(C, name="fesom2_graph_end_")
+      import :: c_ptr, c_int
+      integer(c_int) :: istat
+      type(c_ptr) :: s, graph
+    end subroutine
+    subroutine fesom2_graph_launch(istat, graph, s) bind(C, name="fesom2_graph_launch_")
+      import :: c_ptr, c_int
+      integer(c_int) :: istat
+      type(c_ptr) :: graph, s
+    end subroutine
+    subroutine fesom2_graph_free(graph) bind(C, name="fesom2_graph_free_")
+      import :: c_ptr
+      type(c_ptr) :: graph
+    end subroutine
   end interface
 end module fesom2_accelerate

@@ -143,6 +143,14 @@ void fesom2_upload_(void **mem, void *host_ptr, int *istat);
 /* Release a handle / stream / pinned buffer (the reference never frees). */
 void fesom2_free_(void **mem);
 void fesom2_free_stream_(void **stream);
+/* hipGraph capture of everything the entry points enqueue on *s between begin and end (device-
+ * resident mode; the meshes' plans must exist: run the sequence once or fesom2_prepare_mesh_ first).
+ * launch replays it on *s without host-side work; free releases it.  istat 0 = ok.  Buffer events
+ * (transfer_var_async_) are not waited on inside a capture: order their uploads before the launch. */
+void fesom2_graph_begin_(int *istat, void **s);
+void fesom2_graph_end_(int *istat, void **s, void **graph);
+void fesom2_graph_launch_(int *istat, void **graph, void **s);
+void fesom2_graph_free_(void **graph);
 void fesom2_free_pinned_(void **hostptr);
 /* Device-wide synchronisation and last error string (empty if none). */
 void fesom2_device_sync_(int *istat);

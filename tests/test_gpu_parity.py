@@ -485,3 +485,39 @@ def test_split_by_direction_vlimit(vlimit):
     finally:
         e.free()
         dm.free()
+
+
+def test_graph_replay_matches_oracle():
+    """A split pass captured into a hipGraph (fesom2_graph_begin_/end_) and replayed gives the eager
+    results; a capture that would have to build a mesh plan fails cleanly."""
+    m, f = mesh("127k x 47")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm_v() == 7 and e.post_comm_h() == 9  # builds the plans
+        for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(k)  # pristine inputs again
+        e.sync()
+        with abi.Graph.capture(e.stream) as g:
+            assert e.pre_comm_v() == 7, abi.last_error()
+            assert e.post_comm_h() == 9, abi.last_error()
+        g.launch(e.stream)
+        e.sync()
+        got = {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+        g.free()
+    finally:
+        e.free()
+        dm.free()
+    check_pass(m, got, O.full_pass(m, f))
+    # no plan yet for a fresh mesh: the capture refuses to build one
+    m2, f2 = mesh("8k x 20", True)
+    dm2 = engine.DeviceMesh(m2)
+    e2 = engine.FctAle(dm2, f2)
+    try:
+        with abi.Graph.capture(e2.stream) as g2:
+            assert e2.pre_comm_v() == 0
+            assert "graph capture" in abi.last_error()
+        g2.free()
+    finally:
+        e2.free()
+        dm2.free()
