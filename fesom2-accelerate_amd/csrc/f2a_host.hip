@@ -11,8 +11,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
-#include <atomic>
 #include <tuple>
+#include <unordered_map>
 
 namespace f2a {
 
@@ -76,6 +76,7 @@ Buffer *buf(void **h, const char *name)
         report("invalid handle for %s (not created by this library)", name);
         return nullptr;
     }
+    note_use(b, b->serial);
     return b;
 }
 
@@ -114,15 +115,18 @@ hipStream_t stream_of(void **s)
 Buffer *allocate(void *host, size_t bytes, bool create_event)
 {
     auto *m = new Buffer;
+    m->serial = track_object(m);
     m->host_pointer = host;
     m->size = bytes;
     if (!ok(hipMalloc(&m->device_pointer, bytes ? bytes : 8), "hipMalloc")) {
+        untrack_object(m);
         delete m;
         return nullptr;
     }
     if (create_event) {
         if (!ok(hipEventCreateWithFlags(&m->event, hipEventDisableTiming), "hipEventCreate")) {
             (void)hipFree(m->device_pointer);
+            untrack_object(m);
             delete m;
             return nullptr;
         }
@@ -147,12 +151,19 @@ bool d2h_async(Buffer *b, hipStream_t s)
     return ok(hipMemcpyAsync(b->host_pointer, b->device_pointer, b->size, hipMemcpyDeviceToHost, s), "D2H async");
 }
 
-// Inside a graph capture the buffer events (recorded outside it by transfer_var_async_) are not
-// waited on -- a captured stream may not wait on an event from outside the capture; the caller
-// orders the producers' uploads before the graph launch.
+// The reference waits on the producers' upload events before its kernels (fesom2-accelerate.cu:293,
+// :316, :326).  A captured stream may not wait on an event recorded outside the capture, so inside
+// a capture the wait is recorded instead and fesom2_graph_launch_ issues it on the launch stream
+// before every replay.
 void wait_event(Buffer *b, hipStream_t s)
 {
-    if (b->has_event && !capturing()) (void)hipStreamWaitEvent(s, b->event, 0);
+    if (!b->has_event) return;
+    if (capturing(s)) {
+        if (!defer_event_wait(b, s))
+            report("stream captured outside fesom2_graph_begin_: the wait for a buffer event is dropped");
+        return;
+    }
+    (void)hipStreamWaitEvent(s, b->event, 0);
 }
 
 bool check_levels(int nl, const char *who)
@@ -212,9 +223,120 @@ void resolve_pending()
 
 bool timing_enabled() { return g_timing; }
 
-static std::atomic<bool> g_capturing{false};
-bool capturing() { return g_capturing.load(); }
-void set_capturing(bool on) { g_capturing.store(on); }
+// ----------------------------------------------------------------------------- live objects
+
+namespace {
+std::mutex g_live_mutex;
+std::unordered_map<const void *, uint64_t> g_live;
+uint64_t g_next_serial = 1;
+}  // namespace
+
+uint64_t track_object(const void *p)
+{
+    std::lock_guard<std::mutex> lock(g_live_mutex);
+    const uint64_t s = g_next_serial++;
+    g_live[p] = s;
+    return s;
+}
+
+void untrack_object(const void *p)
+{
+    std::lock_guard<std::mutex> lock(g_live_mutex);
+    g_live.erase(p);
+}
+
+bool object_live(const void *p, uint64_t serial)
+{
+    std::lock_guard<std::mutex> lock(g_live_mutex);
+    auto it = g_live.find(p);
+    return it != g_live.end() && it->second == serial;
+}
+
+// ----------------------------------------------------------------------------- graph captures
+
+namespace {
+struct OpenCapture {
+    hipStream_t origin = nullptr;
+    unsigned long long id = 0;  // hipStreamGetCaptureInfo id, shared by streams forked into it
+    CaptureLog log;
+};
+std::mutex g_cap_mutex;
+std::vector<OpenCapture *> g_caps;
+thread_local OpenCapture *t_cap = nullptr;  // the capture this thread opened
+
+void add_unique(std::vector<CapturedUse> &v, const void *p, uint64_t serial)
+{
+    for (const CapturedUse &u : v)
+        if (u.p == p) return;
+    v.push_back({p, serial});
+}
+}  // namespace
+
+bool capturing(hipStream_t s)
+{
+    if (!s) return false;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
+bool any_capture()
+{
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    return !g_caps.empty();
+}
+
+void note_use(const void *p, uint64_t serial)
+{
+    if (!t_cap) return;
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    add_unique(t_cap->log.uses, p, serial);
+}
+
+bool defer_event_wait(Buffer *b, hipStream_t s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(s, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return false;
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    for (OpenCapture *c : g_caps)
+        if (c->id == id) {
+            add_unique(c->log.waits, b, b->serial);
+            add_unique(c->log.uses, b, b->serial);
+            return true;
+        }
+    return false;
+}
+
+bool capture_open(hipStream_t s)
+{
+    if (t_cap) return false;
+    auto *c = new OpenCapture;
+    c->origin = s;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamGetCaptureInfo(s, &st, &c->id) != hipSuccess || st != hipStreamCaptureStatusActive) {
+        delete c;
+        return false;
+    }
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    g_caps.push_back(c);
+    t_cap = c;
+    return true;
+}
+
+bool capture_close(hipStream_t s, CaptureLog *log)
+{
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    for (size_t k = 0; k < g_caps.size(); k++)
+        if (g_caps[k]->origin == s && s) {
+            OpenCapture *c = g_caps[k];
+            *log = std::move(c->log);
+            g_caps.erase(g_caps.begin() + k);
+            if (t_cap == c) t_cap = nullptr;
+            delete c;
+            return true;
+        }
+    return false;
+}
 
 void timing_begin(const char *name, hipStream_t s, void **token)
 {
@@ -290,7 +412,12 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     std::vector<unsigned short> off(einfo.size());
     int nint = 0;
     const char *cenv = getenv("FESOM2_B3HP_CAP");  // level pairs per block (A/B; default kB3hPackSlots)
-    const int cap = std::max(64, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048));
+    // at least one edge of the deepest kind per block (else no block could take it), and at most
+    // 2048 pairs = a 1024-thread block at two slots per thread (the launch falls back to two slots
+    // per thread whenever one slot per thread would need more than 1024 threads)
+    int lmax = 0;
+    for (const int4 &ei : einfo) lmax = std::max(lmax, ei.z);
+    const int cap = std::max({64, (lmax + 1) / 2, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048)});
     for (int part = 0; part < 2; part++) {
         const int k_end = part ? (int)einfo.size() : n_int;
         int k = part ? n_int : 0;
@@ -304,6 +431,7 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
                 slots += s;
                 k++;
             }
+            if (k == k0) return false;  // unreachable with cap >= ceil(lmax / 2); never loop forever
             desc.push_back(make_int2(k0, k - k0));
         }
         if (!part) nint = (int)desc.size();
@@ -787,8 +915,8 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                 n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0};
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.get();
-    if (capturing()) {  // building a plan copies host <-> device: not inside a graph capture
-        report("a mesh plan would be built during a graph capture: run the sequence once (or "
+    if (any_capture()) {  // building a plan copies with hipMemcpy, which would break an open capture
+        report("a mesh plan would be built while a graph capture is open: run the sequence once (or "
                "fesom2_prepare_mesh_) before fesom2_graph_begin_");
         return nullptr;
     }

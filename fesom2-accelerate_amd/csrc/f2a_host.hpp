@@ -49,12 +49,46 @@ inline T *dptr(Buffer *b)
 inline size_t col_bytes(long cols, int stride) { return (size_t)cols * stride * sizeof(real); }
 bool check_levels(int nl, const char *who);
 
+// ---- live objects (Buffer, halo plan, communicator): a serial per live object, so a graph replay
+//      can refuse to run when something it captured has been freed (or freed and reallocated at
+//      the same address) since the capture.
+uint64_t track_object(const void *p);  // register p, return its fresh serial
+void untrack_object(const void *p);
+bool object_live(const void *p, uint64_t serial);
+// Called by every handle lookup: while this thread has a capture open (fesom2_graph_begin_), p is
+// recorded as used by the graph.  (Eager calls of the same thread on other streams are recorded
+// too; that only makes the replay's liveness check stricter.)
+void note_use(const void *p, uint64_t serial);
+
+// ---- hipGraph capture (fesom2_graph_begin_ / _end_ / _launch_).  Decided per stream: a stream is
+//      captured if it is the origin of an open capture or was forked into one (the halo stream).
+bool capturing(hipStream_t s);
+// some capture opened by fesom2_graph_begin_ is still open (any stream, any thread): plan builds
+// copy with hipMemcpy, which synchronises the blocking streams and would break it
+bool any_capture();
+// What a capture recorded: the objects its calls used, and the buffers whose events (recorded by
+// transfer_var_async_ outside the capture, which a captured stream may not wait on) every replay
+// must wait for before it starts.
+struct CapturedUse {
+    const void *p;
+    uint64_t serial;
+};
+struct CaptureLog {
+    std::vector<CapturedUse> uses, waits;
+};
+// register an open capture whose origin is s (after hipStreamBeginCapture); false if this thread
+// already has one open
+bool capture_open(hipStream_t s);
+// unregister the capture whose origin is s and hand over its log; false if s is not the origin of
+// a capture opened by capture_open
+bool capture_close(hipStream_t s, CaptureLog *log);
+// the captured call on stream s would wait for b's event: record the wait in the log of the
+// capture s belongs to (false if s is not in a capture opened by capture_open)
+bool defer_event_wait(Buffer *b, hipStream_t s);
+
 // ---- per-kernel timing (fesom2_kernel_timing_): HIP events recorded around each launch on the
 //      launch stream while enabled; resolved when the statistics are read.
 bool timing_enabled();
-// a pass is being captured into a hipGraph (fesom2_graph_begin_): no timing events, no plan builds
-bool capturing();
-void set_capturing(bool on);
 void timing_begin(const char *name, hipStream_t s, void **token);
 void timing_end(void *token, hipStream_t s);
 // Launch through `f` with optional timing; reports failures under `name`.
@@ -62,7 +96,7 @@ template <class F>
 bool run(const char *name, hipStream_t s, F &&f)
 {
     void *tok = nullptr;
-    if (timing_enabled() && !capturing()) timing_begin(name, s, &tok);
+    if (timing_enabled() && !capturing(s)) timing_begin(name, s, &tok);
     const bool good = ok(f(), name);
     if (tok) timing_end(tok, s);
     return good;

@@ -21,6 +21,7 @@ struct Buffer {
     size_t size = 0;  // bytes
     hipEvent_t event = nullptr;
     bool has_event = false;
+    uint64_t serial = 0;  // live-object serial (track_object): graph replays check it is unchanged
 };
 
 // One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the

@@ -1426,7 +1426,7 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
             // slots per thread; the 1- and 4-slot forms exist for even L with non-temporal streams only,
             // and the block must cover the capacity for the form actually launched
             int H = env_int("FESOM2_B3HP_H", 2);
-            if ((H != 1 && H != 4) || (L % 2) || !NT) H = 2;
+            if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && mp.b3p_cap > 1024)) H = 2;
             const dim3 grid((unsigned)groups), block((mp.b3p_cap + H - 1) / H);
             if (H == 1) {
                 hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,

@@ -883,6 +883,7 @@ void fesom2_free_(void **mem)
     Buffer *b = buf(mem, "fesom2_free_");
     if (!b) return;
     drop_plans_of(b);
+    untrack_object(b);
     (void)hipFree(b->device_pointer);
     if (b->has_event) (void)hipEventDestroy(b->event);
     b->magic = 0;
@@ -911,12 +912,19 @@ void fesom2_device_sync_(int *istat) { *istat = ok(hipDeviceSynchronize(), "hipD
 // enqueue on *s between begin and end -- kernels, the exchange's fork/join onto the halo stream and
 // its RCCL send/recv -- becomes one graph; launching it replays the sequence without the host-side
 // validation, plan lookups and per-kernel launches.  The meshes' plans must exist already (one
-// ordinary pass, or fesom2_prepare_mesh_).  Kernel timing is off while capturing.
+// ordinary pass, or fesom2_prepare_mesh_).  Kernel timing is off on captured streams.
+//
+// A replay re-runs the captured launches with the arguments read at capture time (buffers, sizes,
+// dt/flux_eps/bignumber/vlimit, ntracers, path and FESOM2_* kernel choices) and does not write
+// alg_state.  Before each replay it waits on the launch stream for the events of the buffers the
+// captured calls would have waited on (transfer_var_async_ uploads, reference :293/:316/:326), and it
+// refuses to run if a buffer, halo plan or communicator the capture used has been freed since.
 struct GraphHandle {
     static constexpr uint32_t kMagic = 0xF2A6A9F1u;
     uint32_t magic = kMagic;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    CaptureLog log;
 };
 
 void fesom2_graph_begin_(int *istat, void **s)
@@ -931,8 +939,17 @@ void fesom2_graph_begin_(int *istat, void **s)
         report("fesom2_graph_begin_: the null stream cannot be captured");
         return;
     }
+    if (capturing(st)) {
+        report("fesom2_graph_begin_: the stream is already being captured");
+        return;
+    }
     if (!ok(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture")) return;
-    f2a::set_capturing(true);
+    if (!capture_open(st)) {
+        report("fesom2_graph_begin_: this thread already has a capture open (end it first)");
+        hipGraph_t g = nullptr;
+        if (hipStreamEndCapture(st, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+        return;
+    }
     *istat = 0;
 }
 
@@ -940,9 +957,14 @@ void fesom2_graph_end_(int *istat, void **s, void **graph)
 {
     *istat = 1;
     *graph = nullptr;
-    f2a::set_capturing(false);
+    const hipStream_t st = stream_of(s);
     auto *g = new GraphHandle;
-    if (!ok(hipStreamEndCapture(stream_of(s), &g->graph), "hipStreamEndCapture") ||
+    if (!capture_close(st, &g->log)) {
+        report("fesom2_graph_end_: the stream has no capture opened by fesom2_graph_begin_");
+        delete g;
+        return;
+    }
+    if (!ok(hipStreamEndCapture(st, &g->graph), "hipStreamEndCapture") ||
         !ok(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0), "hipGraphInstantiate")) {
         if (g->graph) (void)hipGraphDestroy(g->graph);
         delete g;
@@ -960,7 +982,27 @@ void fesom2_graph_launch_(int *istat, void **graph, void **s)
         report("fesom2_graph_launch_: invalid graph handle");
         return;
     }
-    if (ok(hipGraphLaunch(g->exec, stream_of(s)), "hipGraphLaunch")) *istat = 0;
+    for (const CapturedUse &u : g->log.uses)
+        if (!object_live(u.p, u.serial)) {
+            report("fesom2_graph_launch_: a buffer, halo plan or communicator the graph captured has been "
+                   "freed since the capture (capture again)");
+            return;
+        }
+    const hipStream_t st = stream_of(s);
+    for (const CapturedUse &w : g->log.waits) {
+        const Buffer *b = static_cast<const Buffer *>(w.p);
+        if (!ok(hipStreamWaitEvent(st, b->event, 0), "hipStreamWaitEvent(graph launch)")) return;
+    }
+    if (ok(hipGraphLaunch(g->exec, st), "hipGraphLaunch")) *istat = 0;
+}
+
+// objects a graph used / buffer events it waits on before each replay (tests and diagnostics)
+void fesom2_graph_info_(void **graph, int *n_uses, int *n_waits)
+{
+    auto *g = graph && *graph ? static_cast<GraphHandle *>(*graph) : nullptr;
+    const bool valid = g && g->magic == GraphHandle::kMagic;
+    *n_uses = valid ? (int)g->log.uses.size() : -1;
+    *n_waits = valid ? (int)g->log.waits.size() : -1;
 }
 
 void fesom2_graph_free_(void **graph)

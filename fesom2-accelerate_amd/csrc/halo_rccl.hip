@@ -22,11 +22,13 @@ struct Comm {
     uint32_t magic = kMagic;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
+    uint64_t serial = 0;  // track_object
 };
 
 struct HaloPlan {
     static constexpr uint32_t kMagic = 0xF2A4A105u;
     uint32_t magic = kMagic;
+    uint64_t serial = 0;  // track_object
     int L = 0;
     std::vector<int> ranks, scount, rcount, soff, roff;  // offsets in columns
     int nsend = 0, nrecv = 0, max_col = -1;
@@ -58,7 +60,9 @@ Comm *comm_of(void **h)
         report("invalid communicator handle");
         return nullptr;
     }
-    return static_cast<Comm *>(*h);
+    Comm *c = static_cast<Comm *>(*h);
+    note_use(c, c->serial);
+    return c;
 }
 
 HaloPlan *plan_of(void **h)
@@ -67,7 +71,9 @@ HaloPlan *plan_of(void **h)
         report("invalid halo plan handle");
         return nullptr;
     }
-    return static_cast<HaloPlan *>(*h);
+    HaloPlan *p = static_cast<HaloPlan *>(*h);
+    note_use(p, p->serial);
+    return p;
 }
 
 // pack/recv buffers for ntr tracers (grown on first use by a larger batch; the old ones stay in
@@ -108,6 +114,7 @@ void fesom2_comm_init_(void **comm, char *id128, int *rank, int *nranks, int *is
         *comm = nullptr;
         return;
     }
+    c->serial = track_object(c);
     *comm = c;
     *istat = 0;
 }
@@ -116,6 +123,7 @@ void fesom2_comm_free_(void **comm)
 {
     Comm *c = comm_of(comm);
     if (!c) return;
+    untrack_object(c);
     (void)ncclCommDestroy(c->comm);
     c->magic = 0;
     delete c;
@@ -164,6 +172,7 @@ void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_cou
         delete p;
         return;
     }
+    p->serial = track_object(p);
     *plan = p;
     *istat = 0;
 }
@@ -172,6 +181,7 @@ void fesom2_halo_plan_free_(void **plan)
 {
     HaloPlan *p = plan_of(plan);
     if (!p) return;
+    untrack_object(p);
     p->magic = 0;
     delete p;
     *plan = nullptr;

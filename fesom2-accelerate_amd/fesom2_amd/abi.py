@@ -32,6 +32,7 @@ EXPORTS = (
     "fct_ale_post_comm_iter_batched_acc_", "fesom2_exchange_nod_acc_",
     "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_", "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_",
     "fesom2_graph_begin_", "fesom2_graph_end_", "fesom2_graph_launch_", "fesom2_graph_free_",
+    "fesom2_graph_info_",
 )
 
 _dll = None
@@ -170,6 +171,12 @@ class Graph(Handle):
         st = C.c_int(0)
         dll().fesom2_graph_launch_(C.byref(st), self.ref, stream.ref)
         check(st, "fesom2_graph_launch_")
+
+    def info(self):
+        """(objects the replays check are alive, buffer events each replay waits for)."""
+        nu, nw = C.c_int(0), C.c_int(0)
+        dll().fesom2_graph_info_(self.ref, C.byref(nu), C.byref(nw))
+        return nu.value, nw.value
 
     def free(self):
         if self:

@@ -144,13 +144,21 @@ void fesom2_upload_(void **mem, void *host_ptr, int *istat);
 void fesom2_free_(void **mem);
 void fesom2_free_stream_(void **stream);
 /* hipGraph capture of everything the entry points enqueue on *s between begin and end (device-
- * resident mode; the meshes' plans must exist: run the sequence once or fesom2_prepare_mesh_ first).
- * launch replays it on *s without host-side work; free releases it.  istat 0 = ok.  Buffer events
- * (transfer_var_async_) are not waited on inside a capture: order their uploads before the launch. */
+ * resident mode; the meshes' plans must exist: run the sequence once or fesom2_prepare_mesh_ first;
+ * one open capture per thread, ended on the stream it began on).  launch replays it on *s without
+ * host-side work; free releases it.  istat 0 = ok.
+ * A replay reuses what the calls read at capture time (handles, sizes, dt, flux_eps, bignumber,
+ * vlimit, ntracers, path/FESOM2_* choices) and does not update alg_state.  Before each replay the
+ * launch stream waits for the events of the buffers the captured calls wait on (transfer_var_async_
+ * uploads with record_event, reference :293/:316/:326).  launch fails (istat 1) if a buffer, halo
+ * plan or communicator the capture used has been freed since.  While any capture is open, calls
+ * that would build a new mesh plan fail. */
 void fesom2_graph_begin_(int *istat, void **s);
 void fesom2_graph_end_(int *istat, void **s, void **graph);
 void fesom2_graph_launch_(int *istat, void **graph, void **s);
 void fesom2_graph_free_(void **graph);
+/* Objects a graph's replays check (*n_uses) and buffer events they wait on (*n_waits); -1 = invalid. */
+void fesom2_graph_info_(void **graph, int *n_uses, int *n_waits);
 void fesom2_free_pinned_(void **hostptr);
 /* Device-wide synchronisation and last error string (empty if none). */
 void fesom2_device_sync_(int *istat);
