@@ -92,9 +92,12 @@ def kernel_bytes(s, ntr=1):
     # area shared), then c-horizontal alone (del_h rw, adf_h; area shared)
     p1v = p1 + ntr * 8 * (cn + 2 * cn) + 8 * 3 * cn
     p2h = ntr * 8 * (2 * cn + ce) + 8 * cn + 4 * N + ints_edges
+    # c-horizontal with b3h folded in: raw adf_h read, limited adf_h written once, plus/minus of both
+    # endpoints (owned + halo columns), del_h rw; area shared
+    p2hf = ntr * 8 * (2 * cn + 2 * ce + 2 * (cn + ch)) + 8 * cn + 4 * N + ints_edges + 4 * E
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
-            "fct_ale_p1v": p1v, "fct_ale_p2h": p2h,
+            "fct_ale_p1v": p1v, "fct_ale_p2h": p2h, "fct_ale_p2h_b3h": p2hf,
             "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 

@@ -377,6 +377,44 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
     }
 }
 
+// Edge gathers with the b3-horizontal limiter applied in-thread: for kBatch edges at a time the raw
+// flux and the other endpoint's plus/minus are loaded, then f(c, limited flux, second) runs in
+// ascending edge order.  (pn, mn: this node's plus/minus at the thread's levels.)
+template <int C, int kBatch, bool ODD = false, class F>
+__device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                                  const real *__restrict__ adf_h,
+                                                  const real *__restrict__ plus,
+                                                  const real *__restrict__ minus, const real (&pn)[C],
+                                                  const real (&mn)[C], int z0, int L, F &&f, bool last1 = false)
+{
+    for (int k0 = e0; k0 < e1; k0 += kBatch) {
+        EdgeRef er[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) er[k] = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
+        real h[kBatch][C], po[kBatch][C], mo[kBatch][C];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < (er[k].code >> 1)) {
+                ldo<C, ODD>(adf_h + (size_t)er[k].edge * L + z0, h[k], last1);
+                ldo<C, ODD>(plus + (size_t)er[k].other * L + z0, po[k], last1);
+                ldo<C, ODD>(minus + (size_t)er[k].other * L + z0, mo[k], last1);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const int lev = er[k].code >> 1, second = er[k].code & 1;
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                if (z0 + c >= lev) continue;
+                // docs/refactoring.md:246-257 with (n1, n2) = (other, this) when second
+                const real ae = second ? b3h_factor(h[k][c], po[k][c], mo[k][c], pn[c], mn[c])
+                                       : b3h_factor(h[k][c], pn[c], mn[c], po[k][c], mo[k][c]);
+                f(c, ae * h[k][c], second, k0 + k);
+            }
+        }
+    }
+}
+
 // Stage the block's NodeRec records (one coalesced 16-byte-per-thread sweep) into LDS after
 // `lds_base`; ends with a block barrier.
 __device__ __forceinline__ const NodeRec *stage_records(const NodeRec *__restrict__ recs, int first, int ncol,

@@ -166,6 +166,10 @@ struct P2Args {
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
+// c-horizontal with b3-horizontal folded in (split pass, FESOM2_P2H_FUSE): a.edge_cnt = the plan's
+// per-edge arrival counters (never reset: two arrivals per edge per pass), a.n_owned set, every node
+// of mp.max_degree <= kMaxFusedDegree; edges without an owned endpoint are not touched
+hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal folded into the node kernel (a.edge_cnt zeroed, mp.max_degree <= kMaxFusedDegree):
 // every endpoint limits its edges' fluxes itself for c-horizontal, and the endpoint that arrives
 // last at an edge's counter -- after its block has read the raw column -- writes the limited

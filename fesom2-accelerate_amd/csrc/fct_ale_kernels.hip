@@ -630,6 +630,113 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
+// Phase 2, horizontal half with b3-horizontal folded in (FESOM2_P2H_FUSE): c-horizontal over the
+// node's edges with each raw fct_adf_h limited in-thread from both endpoints' plus/minus, so the
+// separate b3h pass (read + write of fct_adf_h, plus/minus gathers) and p2h's re-read of the limited
+// flux become one read of the raw flux per endpoint.  The limited flux is stored in place once, by
+// the endpoint that reads the raw flux last: after the block barrier (all raw reads of the block
+// done) one thread per (column, edge) bumps the edge's arrival counter -- counters only ever grow by
+// the edge's owned endpoints, two per pass, so an odd old value marks the second arriver and no
+// reset is needed -- and a halo endpoint never arrives, so the owned one writes.  The writer loads
+// the raw flux and the other endpoint's plus/minus again (L2-resident: its block just read them).
+template <int C, int KB, bool NT, bool ODD>
+__global__ __launch_bounds__(1024) void k_p2hf(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G] | writer masks[G]
+    const int L = a.nl - 1, S = (L + C - 1) / C;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.del_h += tr * a.tr.node;
+        a.adf_h += tr * a.tr.edge;
+        a.edge_cnt += (size_t)tr * mp.n_edges;
+    }
+    unsigned *wmask = reinterpret_cast<unsigned *>(reinterpret_cast<NodeRec *>(lds) + G);
+    if ((int)threadIdx.x < G) wmask[threadIdx.x] = 0u;
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);  // (its barrier also orders wmask)
+    int j, u;
+    slot_of(threadIdx.x, S, invS, j, u);
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int nw = col ? max(0, min(C, ni.Ln - z0)) : 0;
+    const int ne = col ? ni.e1 - ni.e0 : 0;
+    real pn[C], mn[C], dh[C];
+    size_t b = 0;
+    if (nw > 0) {
+        b = (size_t)ni.n * L + z0;
+        const size_t ab = (size_t)ni.n * a.nl + z0;
+        ldo<C, ODD>(a.plus + b, pn, last1);
+        ldo<C, ODD>(a.minus + b, mn, last1);
+        ldo_s<C, NT, ODD>(a.del_h + b, dh, last1);
+        real dta[C];
+        if constexpr (C == 2) {  // area: one 16-B load at 8-B alignment (ld_nl)
+            const f2a_d2u t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2a_d2u *>(a.area + ab))
+                                 : *reinterpret_cast<const f2a_d2u *>(a.area + ab);
+            dta[0] = a.dt / t.x;
+            dta[1] = nw >= 2 ? a.dt / t.y : 0.;
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+        }
+        auto add = [&](int c, real h, int second, int) {
+            dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+        };
+        for_edges_limited<C, KB, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                      add, last1);
+        if (ne > kRecEdge)
+            for_edges_limited<C, KB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                          add, last1);
+    }
+    __syncthreads();  // every raw fct_adf_h read of the block is done
+    const int abl = c_ablate;  // timing-only experiments: 16 static writer (racy), 32 no writer
+    for (int k = u; k < ne; k += S) {
+        const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+        if ((abl & 16) ? !(er.code & 1)
+                       : (er.other >= a.n_owned || (atomicAdd(reinterpret_cast<unsigned *>(a.edge_cnt) + er.edge, 1u) & 1u)))
+            atomicOr(&wmask[j], 1u << k);
+    }
+    __syncthreads();
+    if (nw <= 0) return;
+    stv_s<C, NT>(a.del_h + b, dh, nw);
+    unsigned mine = (abl & 32) ? 0u : wmask[j];
+    while (mine) {  // the edges this column writes, KB at a time
+        int ks[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            ks[q] = mine ? __builtin_ctz(mine) : -1;
+            if (mine) mine &= mine - 1;
+        }
+        EdgeRef er[KB];
+        real h[KB][C], po[KB][C], mo[KB][C];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            er[q] = ks[q] < 0 ? EdgeRef{0, 0, 0} : (ks[q] < kRecEdge ? recs[j].edge[ks[q]] : mp.p_edges[ni.e0 + ks[q]]);
+            if (z0 < (er[q].code >> 1)) {
+                ldo_s<C, NT, ODD>(a.adf_h + (size_t)er[q].edge * L + z0, h[q], last1);
+                ldo<C, ODD>(a.plus + (size_t)er[q].other * L + z0, po[q], last1);
+                ldo<C, ODD>(a.minus + (size_t)er[q].other * L + z0, mo[q], last1);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            const int lev = er[q].code >> 1, second = er[q].code & 1;
+            if (z0 >= lev) continue;
+            real out[C];
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                out[c] = (second ? b3h_factor(h[q][c], po[q][c], mo[q][c], pn[c], mn[c])
+                                 : b3h_factor(h[q][c], pn[c], mn[c], po[q][c], mo[q][c])) * h[q][c];
+            stv_s<C, NT>(a.adf_h + (size_t)er[q].edge * L + z0, out, min(C, lev - z0));
+        }
+    }
+}
+
 // Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
 template <int C>
 __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, int n_edges, int L,
@@ -1326,6 +1433,29 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     }
     if (NT) F2A_LAUNCH_GROUPS((k_p2h<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p2h<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+}
+
+hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1;
+    const bool odd = odd_pairs(L);
+    const int C = odd ? 2 : levels_per_thread(L), S = (L + C - 1) / C, G = group_columns(S);
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec) + G * sizeof(unsigned);
+    const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;
+    const int KB = env_int("FESOM2_P2HF_KB", 2);
+    if (odd) {
+        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (C == 2) {
+        if (KB == 4) F2A_LAUNCH_GROUPS((k_p2hf<2, 4, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 1) F2A_LAUNCH_GROUPS((k_p2hf<2, 1, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    F2A_LAUNCH_GROUPS((k_p2hf<1, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)

@@ -327,44 +327,6 @@ __global__ __launch_bounds__(1024) void k_p1s(MeshPlanDev mp, P1Args a, int G, f
     stv<C>(a.minus + b, om, nw);
 }
 
-// Edge gathers with the b3-horizontal limiter applied in-thread: for kBatch edges at a time the raw
-// flux and the other endpoint's plus/minus are loaded, then f(c, limited flux, second) runs in
-// ascending edge order.  (pn, mn: this node's plus/minus at the thread's levels.)
-template <int C, int kBatch, class F>
-__device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ edges, int e0, int e1,
-                                                  const real *__restrict__ adf_h,
-                                                  const real *__restrict__ plus,
-                                                  const real *__restrict__ minus, const real (&pn)[C],
-                                                  const real (&mn)[C], int z0, int L, F &&f)
-{
-    for (int k0 = e0; k0 < e1; k0 += kBatch) {
-        EdgeRef er[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) er[k] = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
-        real h[kBatch][C], po[kBatch][C], mo[kBatch][C];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            if (z0 < (er[k].code >> 1)) {
-                ldv<C>(adf_h + (size_t)er[k].edge * L + z0, h[k]);
-                ldv<C>(plus + (size_t)er[k].other * L + z0, po[k]);
-                ldv<C>(minus + (size_t)er[k].other * L + z0, mo[k]);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            const int lev = er[k].code >> 1, second = er[k].code & 1;
-#pragma unroll
-            for (int c = 0; c < C; c++) {
-                if (z0 + c >= lev) continue;
-                // docs/refactoring.md:246-257 with (n1, n2) = (other, this) when second
-                const real ae = second ? b3h_factor(h[k][c], po[k][c], mo[k][c], pn[c], mn[c])
-                                       : b3h_factor(h[k][c], pn[c], mn[c], po[k][c], mo[k][c]);
-                f(c, ae * h[k][c], second);
-            }
-        }
-    }
-}
-
 // Phase 2 with b3-horizontal folded in (b3h + b3v + cv + ch, see launch_p2_fused_b3h).  Each
 // endpoint limits its edges' raw fluxes for its own c-horizontal; after the block barrier (every
 // raw fct_adf_h read of the block done) one thread per (column, edge) bumps the edge's counter, and
@@ -448,7 +410,7 @@ __global__ __launch_bounds__(1024) void k_p2f(MeshPlanDev mp, P2Args a, int G, f
                 tv = tv + lo[c] * hnn[c];
                 dv[c] = tv + (lim[c] - lim[c + 1]) * dta[c];
             }
-            auto add = [&](int c, real h, int second) {
+            auto add = [&](int c, real h, int second, int) {
                 dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
             };
             for_edges_limited<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L, add);

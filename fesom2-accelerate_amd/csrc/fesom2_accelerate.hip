@@ -652,6 +652,35 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), nullptr, nullptr, nullptr, nullptr,
                   dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    // FESOM2_P2H_FUSE=1: b3-horizontal folded into the c-horizontal node kernel (k_p2hf, arrival
+    // counters decide which endpoint stores the limited flux)
+    const char *fz = getenv("FESOM2_P2H_FUSE");
+    if (fz && atoi(fz) != 0 && d.max_degree <= f2a::kMaxFusedDegree && (int)plan->owner_cum.size() == N + 1) {
+        a.n_owned = N;
+        const bool fresh = plan->cnt_tracers < ntr;
+        a.edge_cnt = plan_edge_counters(plan, ntr);
+        if (!a.edge_cnt ||
+            (fresh && !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st),
+                          "hipMemsetAsync(edge counters)")))
+            return;
+        const int owned_edges = plan->owner_cum.back();  // edges with an owned endpoint come first
+        if (!run("fct_ale_p2h_b3h", st, [&] { return f2a::launch_p2hf(d, a, st); })) return;
+        if (exch) {
+            if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
+            a.nodes = d.p2_rec + n_first;
+            a.count = N - n_first;
+            if (!run("fct_ale_p2h_b3h_boundary", st, [&] { return f2a::launch_p2hf(d, a, st); })) return;
+        }
+        if (owned_edges < E &&  // edges without an owned endpoint (none in a FESOM partition)
+            !run("fct_ale_b3_horizontal", st, [&] {
+                return f2a::launch_b3h_edges(d.p_edge_owner + owned_edges, E - owned_edges, NL, dptr<real>(bplus),
+                                             dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
+            }))
+            return;
+        *alg_state = 9;
+        if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
+        return;
+    }
     // FESOM2_B3H_NODE=1 (no exchange): b3h node-centric over the owner order -- exact, measured
     // 3-17 % slower than the edge-centric two-groups-per-block kernel
     const char *b3n = getenv("FESOM2_B3H_NODE");

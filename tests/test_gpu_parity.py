@@ -434,7 +434,34 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "1"}, {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "3"},
                {"FESOM2_B3H_NODE": "1", "FESOM2_ODD_PAIR": "0"}, {"FESOM2_B3H_PACK": "0"},
                {"FESOM2_B3H_PACK": "1", "FESOM2_B3H_NT": "0"},
-               {"FESOM2_B3HP_H": "1"}, {"FESOM2_B3HP_H": "4"}, {"FESOM2_B3HP_CAP": "100"}]
+               {"FESOM2_B3HP_H": "1"}, {"FESOM2_B3HP_H": "4"}, {"FESOM2_B3HP_CAP": "100"},
+               {"FESOM2_P2H_FUSE": "1"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "1"},
+               {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "4"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_NT": "0"},
+               {"FESOM2_P2H_FUSE": "1", "FESOM2_ODD_PAIR": "0"}]
+
+
+@pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
+@pytest.mark.parametrize("full", [False, True])
+def test_fused_b3h_level_counts_and_repeats(nl, full, monkeypatch):
+    """FESOM2_P2H_FUSE=1 (b3h folded into c-horizontal, arrival counters that are never reset): three
+    passes on the same plan, inputs re-uploaded before each, every one exact."""
+    monkeypatch.setenv("FESOM2_P2H_FUSE", "1")
+    m = synth.make_mesh(40, 14, nl, full_depth=full)
+    f = synth.make_fields(m)
+    want = O.full_pass(m, f)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        for _ in range(3):
+            for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+                e.upload(k)
+            assert e.pre_comm_v() == 7, abi.last_error()
+            assert e.post_comm_h() == 9, abi.last_error()
+            e.sync()
+            check_pass(m, {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}, want)
+    finally:
+        e.free()
+        dm.free()
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))

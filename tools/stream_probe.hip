@@ -1,0 +1,147 @@
+// stream_probe.hip -- ceiling of p1v's stream pattern on MI355X (no gathers, no arithmetic to speak of).
+//
+// p1v (fct_ale_kernels.hip k_p1<..., VERT>) reads 11.5 and writes 4 doubles per wet cell from 13
+// arrays (ttf, LO, adf_v, area_inv, area, hnode, hnode_new, del_v, 3 x adf_h) and writes plus, minus,
+// adf_v, del_v.  This probe moves the same bytes:
+//   copy   flat 16-B/lane copy of one array (the guide's 6.29 TB/s float4 copy)
+//   flat   13 reads + 4 writes per level pair, thread = pair, linear order
+//   cols   the same in p1v's block shape: G = 8 columns x L/2 threads, XCD-swizzled tiles, the three
+//          stride-nl arrays at nl = L+1 (8-byte aligned 16-B loads), adf_h as three columns per node
+// Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe tools/stream_probe.hip
+// Run:   ./stream_probe [nodes=1200000] [L=80]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef double d2 __attribute__((ext_vector_type(2), aligned(8)));
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+struct Arrays {
+    const double *ttf, *LO, *adfv, *ainv, *area, *hn, *hnn, *dv, *adfh;
+    double *plus, *minus, *adfv_o, *dv_o;
+};
+
+__device__ __forceinline__ d2 ld(const double *p) { return *reinterpret_cast<const d2 *>(p); }
+__device__ __forceinline__ void st(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
+
+__global__ __launch_bounds__(256) void k_copy(const d2 *__restrict__ a, d2 *__restrict__ b, long n)
+{
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+
+// thread = level pair i of the flat (Cn) arrays
+__global__ __launch_bounds__(256) void k_flat(Arrays a, long npairs)
+{
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const long b = 2 * i;
+    d2 s = ld(a.ttf + b) + ld(a.LO + b) + ld(a.adfv + b) + ld(a.ainv + b) + ld(a.area + b) + ld(a.hn + b) +
+           ld(a.hnn + b) + ld(a.dv + b);
+    d2 h = ld(a.adfh + 3 * b) + ld(a.adfh + 3 * b + 2) + ld(a.adfh + 3 * b + 4);
+    st(a.plus + b, s);
+    st(a.minus + b, h);
+    st(a.adfv_o + b, s - h);
+    st(a.dv_o + b, s + h);
+}
+
+__device__ __forceinline__ int xcd_tile(int b, int G)
+{
+    const int q = G >> 3, r = G & 7, x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+}
+
+// p1v's shape: block = G columns x S = L/2 slots; node columns n*L, stride-nl arrays n*(L+1),
+// adf_h: three edge columns per node (edge e = 3n + k, column e*L)
+__global__ __launch_bounds__(1024) void k_cols(Arrays a, int nodes, int L, int G)
+{
+    const int S = L / 2, t = threadIdx.x, j = t / S, u = t - j * S;
+    const int n = xcd_tile(blockIdx.x, gridDim.x) * G + j;
+    if (j >= G || n >= nodes) return;
+    const int z0 = 2 * u, nl = L + 1;
+    const size_t b = (size_t)n * L + z0, ab = (size_t)n * nl + z0;
+    d2 s = ld(a.ttf + b) + ld(a.LO + b) + ld(a.adfv + ab) + ld(a.ainv + ab) + ld(a.area + ab) + ld(a.hn + b) +
+           ld(a.hnn + b) + ld(a.dv + b);
+    const size_t e = (size_t)3 * n * L + z0;
+    d2 h = ld(a.adfh + e) + ld(a.adfh + e + L) + ld(a.adfh + e + 2 * L);
+    st(a.plus + b, s);
+    st(a.minus + b, h);
+    st(a.adfv_o + ab, s - h);
+    st(a.dv_o + b, s + h);
+}
+
+int main(int argc, char **argv)
+{
+    const long nodes = argc > 1 ? atol(argv[1]) : 1200000;
+    const int L = argc > 2 ? atoi(argv[2]) : 80;
+    const long cn = nodes * L, cnl = nodes * (L + 1);
+    std::vector<double *> bufs;
+    auto alloc = [&](long n) {
+        double *p;
+        CHECK(hipMalloc(&p, n * sizeof(double)));
+        CHECK(hipMemset(p, 0, n * sizeof(double)));
+        bufs.push_back(p);
+        return p;
+    };
+    Arrays a;
+    a.ttf = alloc(cn);
+    a.LO = alloc(cn);
+    a.adfv = alloc(cnl);
+    a.ainv = alloc(cnl);
+    a.area = alloc(cnl);
+    a.hn = alloc(cn);
+    a.hnn = alloc(cn);
+    a.dv = alloc(cn);
+    a.adfh = alloc(3 * cn);
+    a.plus = alloc(cn);
+    a.minus = alloc(cn);
+    a.adfv_o = const_cast<double *>(a.adfv);  // in place, as p1v
+    a.dv_o = const_cast<double *>(a.dv);
+    double *src = alloc(4 * cn), *dst = alloc(4 * cn);
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const double bytes_p1 = 8.0 * cn * (8 + 3 + 4);  // 8 own + 3 adf_h reads, 4 writes per cell
+    auto timeit = [&](const char *name, double bytes, auto launch) {
+        for (int w = 0; w < 3; w++) launch();
+        CHECK(hipDeviceSynchronize());
+        const int reps = 20;
+        CHECK(hipEventRecord(e0));
+        for (int r = 0; r < reps; r++) launch();
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        printf("%-28s %8.3f ms  %7.1f GB  %6.2f TB/s\n", name, ms, bytes / 1e9, bytes / (ms * 1e-3) / 1e12);
+        fflush(stdout);
+    };
+    const long n2 = 2 * cn;  // d2 elements of the copy
+    timeit("copy (16 B/lane)", 2.0 * 16 * n2, [&] {
+        hipLaunchKernelGGL(k_copy, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, 0, (const d2 *)src, (d2 *)dst, n2);
+    });
+    const long np = cn / 2;
+    timeit("flat 11R+4W", bytes_p1, [&] {
+        hipLaunchKernelGGL(k_flat, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, 0, a, np);
+    });
+    for (int G : {4, 8, 16, 24}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "cols G=%d 11R+4W", G);
+        const int thr = ((G * (L / 2) + 63) / 64) * 64;
+        timeit(nm, bytes_p1, [&] {
+            hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G);
+        });
+    }
+    for (double *p : bufs) CHECK(hipFree(p));
+    return 0;
+}
