@@ -70,18 +70,22 @@ def mesh_stats(m):
     return dict(N=m.N, E=m.E, T=m.T, cn=cn, cn_halo=cn_halo, ce=ce, ring=ring)
 
 
-def kernel_bytes(s, ntr=1):
+def kernel_bytes(s, ntr=1, split=False):
     """Algorithmic HBM bytes per launch of each kernel of the fused pass (each array element read
     or written once; DESIGN.md §4 derives these).  ntr batched tracers: per-tracer arrays ntr
-    times, mesh fields (area_inv; area, hnode, hnode_new) and index arrays once."""
+    times, mesh fields (area_inv; area, hnode, hnode_new) and index arrays once.  split: the
+    direction-split pass, where p1v limits the block-internal edges (s["ice"] edge cells, s["nie"]
+    edges: their limited fct_adf_h is written by p1v, their raw flux re-read from L2) and b3h runs
+    on the other edges."""
     N, E, T, cn, ch, ce, ring = s["N"], s["E"], s["T"], s["cn"], s["cn_halo"], s["ce"], s["ring"]
+    ice, nie = (s.get("ice", 0), s.get("nie", 0)) if split else (0, 0)
     cn1 = cn + N  # fct_adf_v columns carry the bottom interface too
     ints_edges = 4 * (N + 1) + 16 * 2 * E      # node->edge CSR (EdgeRef = 16 B, two per edge)
     # p1: ttf, LO (owned + halo, cluster gathers), adf_v, adf_h, plus/minus written; area_inv shared
     p1 = ntr * 8 * (2 * (cn + ch) + cn1 + ce + 2 * cn) + 8 * cn + \
         4 * N + ints_edges + 4 * (N + 1) + 8 * ring + 4 * N
     # b3h: adf_h read + written, plus/minus of both endpoints
-    b3h = ntr * 8 * (2 * ce + 2 * (cn + ch)) + 16 * E + 4 * T
+    b3h = ntr * 8 * (2 * (ce - ice) + 2 * (cn + ch)) + 16 * (E - nie) + 4 * T
     # p2: plus, minus, adf_v (r + w), del_v (r + w), del_h (r + w), ttf, LO, adf_h; area, hnode,
     # hnode_new shared
     p2 = ntr * 8 * (9 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
@@ -90,7 +94,7 @@ def kernel_bytes(s, ntr=1):
     p2f = p2 + ntr * 8 * ce
     # split by direction: phase 1 + b3v/cv (adds the limited adf_v write, del_v rw; hnode, hnode_new,
     # area shared), then c-horizontal alone (del_h rw, adf_h; area shared)
-    p1v = p1 + ntr * 8 * (cn + 2 * cn) + 8 * 3 * cn
+    p1v = p1 + ntr * 8 * (cn + 2 * cn + ice) + 8 * 3 * cn + 16 * nie
     p2h = ntr * 8 * (2 * cn + ce) + 8 * cn + 4 * N + ints_edges
     # c-horizontal with b3h folded in: raw adf_h read, limited adf_h written once, plus/minus of both
     # endpoints (owned + halo columns), del_h rw; area shared
@@ -325,6 +329,8 @@ def main():
     abi.set_path("stepwise" if args.path == "stepwise" else "fused")
     dm = engine.DeviceMesh(m)
     dm.prepare()
+    mi = dm.info()
+    mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
     e = engine.FctAle(dm, f, copy=False) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
     stream = e.stream
 
@@ -459,7 +465,8 @@ def main():
 
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
     s = mesh_stats(m)
-    kb = kernel_bytes(s, args.tracers)
+    s.update(mesh_info)
+    kb = kernel_bytes(s, args.tracers, split=args.path == "split")
     per_kernel = {}
     for name, (cnt, tot) in stats.items():
         avg = tot / max(cnt, 1)

@@ -404,13 +404,14 @@ namespace f2a {
 
 // ----------------------------------------------------------------------------- plans
 
-// Packed b3h blocks (MeshPlanDev::b3p_*): greedy over the edge list, separately for [0, n_int) and
-// [n_int, E) so the exchange-overlap split keeps working.
-static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_int)
+// Packed b3h blocks (MeshPlanDev::b3p_*): greedy over the edge list, separately for the ranges
+// [0, n_ext), [n_ext, n_int) and [n_int, E) so the exchange-overlap split and the p1v-internal edges
+// keep their own descriptors.
+static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_ext, int n_int)
 {
     std::vector<int2> desc;
     std::vector<unsigned short> off(einfo.size());
-    int nint = 0;
+    int ends[3] = {0, 0, 0};
     const char *cenv = getenv("FESOM2_B3HP_CAP");  // level pairs per block (A/B; default kB3hPackSlots)
     // at least one edge of the deepest kind per block (else no block could take it), and at most
     // 2048 pairs = a 1024-thread block at two slots per thread (the launch falls back to two slots
@@ -418,9 +419,10 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     int lmax = 0;
     for (const int4 &ei : einfo) lmax = std::max(lmax, ei.z);
     const int cap = std::max({64, (lmax + 1) / 2, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048)});
-    for (int part = 0; part < 2; part++) {
-        const int k_end = part ? (int)einfo.size() : n_int;
-        int k = part ? n_int : 0;
+    const int bounds[4] = {0, n_ext, n_int, (int)einfo.size()};
+    for (int part = 0; part < 3; part++) {
+        int k = bounds[part];
+        const int k_end = bounds[part + 1];
         while (k < k_end) {
             const int k0 = k;
             int slots = 0;
@@ -434,11 +436,12 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
             if (k == k0) return false;  // unreachable with cap >= ceil(lmax / 2); never loop forever
             desc.push_back(make_int2(k0, k - k0));
         }
-        if (!part) nint = (int)desc.size();
+        ends[part] = (int)desc.size();
     }
     d.b3p_desc = plan->mem.upload(desc);
     d.b3p_off = plan->mem.upload(off);
-    d.b3p_nint = nint;
+    d.b3p_next = ends[0];
+    d.b3p_nint = ends[1];
     d.b3p_cap = cap;
     d.b3p_ndesc = (int)desc.size();
     return desc.empty() || (d.b3p_desc && d.b3p_off);
@@ -812,10 +815,52 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 fprintf(stderr, "fesom2-accelerate: wavefront G=%d tiles=%d cross edges=%zu deps/tile %.2f\n", WG, ntiles,
                         cross.size(), (double)deps.size() / std::max(ntiles, 1));
         }
-        // interior / boundary split for the exchange overlap (stable: processing order kept)
+        // interior / boundary split for the exchange overlap (stable: processing order kept), the
+        // interior part split again into edges crossing p1v blocks and edges inside one p1v block
+        // (both endpoints among the same int_G positions: p1v limits those itself, see int_ptr)
         auto interior_edge = [&](const int4 &ei) { return ei.x < n_owned && ei.y < n_owned; };
         std::stable_partition(einfo.begin(), einfo.end(), interior_edge);
         d.n_edge_interior = (int)std::count_if(einfo.begin(), einfo.end(), interior_edge);
+        if (!getenv("FESOM2_P1V_B3H") || atoi(getenv("FESOM2_P1V_B3H")) != 0) {
+            const int IG = p1v_group_columns(nl);
+            std::vector<int> pos(n_owned);
+            for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
+            auto internal = [&](const int4 &ei) { return pos[ei.x] / IG == pos[ei.y] / IG; };
+            const auto mid = std::stable_partition(einfo.begin(), einfo.begin() + d.n_edge_interior,
+                                                   [&](const int4 &ei) { return !internal(ei); });
+            d.n_ext_interior = (int)(mid - einfo.begin());
+            const int nblk = (n_owned + IG - 1) / IG;
+            std::vector<int> iptr(nblk + 1, 0);
+            std::vector<int4> iedges;
+            for (int k = d.n_ext_interior; k < d.n_edge_interior; k++) iptr[pos[einfo[k].x] / IG + 1]++;
+            int most = 0;
+            for (int b = 0; b < nblk; b++) {
+                most = std::max(most, iptr[b + 1]);
+                iptr[b + 1] += iptr[b];
+            }
+            iedges.resize(iptr[nblk]);
+            std::vector<int> fill(iptr.begin(), iptr.end() - 1);
+            for (int k = d.n_ext_interior; k < d.n_edge_interior; k++) {
+                const int4 ei = einfo[k];
+                const int b = pos[ei.x] / IG;
+                // {edge, column of edges(1,e), column of edges(2,e), lev}: einfo keeps edges(1/2,e) order
+                iedges[fill[b]++] = make_int4(ei.w, pos[ei.x] - b * IG, pos[ei.y] - b * IG, ei.z);
+            }
+            if (most <= kMaxInternal && nblk > 0 && !iedges.empty()) {
+                d.int_G = IG;
+                for (const int4 &ie : iedges) plan->int_cells += ie.w;
+                d.int_ptr = plan->mem.upload(iptr);
+                d.int_edges = plan->mem.upload(iedges);
+                if (!d.int_ptr || !d.int_edges) return fail("device allocation for the internal edge lists failed");
+            } else {  // nothing to gain, or a block with too many: every interior edge crosses
+                d.n_ext_interior = d.n_edge_interior;
+            }
+            if (getenv("FESOM2_PLAN_STATS"))
+                fprintf(stderr, "fesom2-accelerate: p1v G=%d internal edges %d of %d interior (max %d per block)\n", IG,
+                        d.n_edge_interior - d.n_ext_interior, d.n_edge_interior, most);
+        } else {
+            d.n_ext_interior = d.n_edge_interior;
+        }
         std::vector<NodeRec> recs(n_owned);
         for (int k = 0; k < n_owned; k++) {
             NodeRec &r = recs[k];
@@ -878,15 +923,15 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
         d.p_edge_info = plan->mem.upload(einfo);
         if (!d.node_info || !d.node_rec || !d.p2_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info ||
-            !build_b3h_pack(plan.get(), d, einfo, d.n_edge_interior))
+            !build_b3h_pack(plan.get(), d, einfo, d.n_ext_interior, d.n_edge_interior))
             return fail("device allocation for the processing order failed");
     } else if (n_edges > 0) {
         std::vector<int4> einfo(n_edges);
         for (int e = 0; e < n_edges; e++)
             einfo[e] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
-        d.n_edge_interior = n_edges;
+        d.n_edge_interior = d.n_ext_interior = n_edges;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.p_edge_info || !build_b3h_pack(plan.get(), d, einfo, n_edges))
+        if (!d.p_edge_info || !build_b3h_pack(plan.get(), d, einfo, n_edges, n_edges))
             return fail("device allocation for the edge list failed");
     }
     return plan;
@@ -964,9 +1009,24 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
         report("invalid mesh: %s", err.c_str());
         return nullptr;
     }
+    plan->serial = track_object(plan.get());
     const Plan *p = plan.get();
     g_plans[key] = std::move(plan);
     return p;
+}
+
+void mark_internal(Buffer *adf_h, const Plan *plan)
+{
+    adf_h->int_plan = plan;
+    adf_h->int_serial = plan ? plan->serial : 0;
+}
+
+const Plan *take_internal(Buffer *adf_h)
+{
+    const void *p = adf_h->int_plan;
+    const uint64_t serial = adf_h->int_serial;
+    adf_h->int_plan = nullptr;
+    return p && object_live(p, serial) ? static_cast<const Plan *>(p) : nullptr;
 }
 
 void drop_plans_of(const Buffer *b)
@@ -975,10 +1035,12 @@ void drop_plans_of(const Buffer *b)
     for (auto it = g_plans.begin(); it != g_plans.end();) {
         const PlanKey &k = it->first;
         if (std::get<0>(k) == b || std::get<1>(k) == b || std::get<2>(k) == b || std::get<3>(k) == b ||
-            std::get<4>(k) == b || std::get<5>(k) == b || std::get<6>(k) == b)
+            std::get<4>(k) == b || std::get<5>(k) == b || std::get<6>(k) == b) {
+            untrack_object(it->second.get());
             it = g_plans.erase(it);
-        else
+        } else {
             ++it;
+        }
     }
 }
 

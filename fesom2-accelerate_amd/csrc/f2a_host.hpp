@@ -128,6 +128,8 @@ struct HostMesh {  // host views of the connectivity a plan is built from (nullp
 struct Plan {
     MeshPlanDev dev;
     DeviceArrays mem;
+    uint64_t serial = 0;  // track_object (fct_adf_h's internal-edge marker refers to a plan)
+    long long int_cells = 0;  // edge cells of the block-internal edges p1v limits
     bool has_ring = false;
     int lmax_edges = 0;
     std::vector<int> owner_cum;  // [n_owned + 1]: edges owned by processing positions < k
@@ -158,6 +160,12 @@ struct MeshHandles {
 const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
                      bool with_ring);
 void drop_plans_of(const Buffer *b);
+// fct_adf_h's internal-edge marker (Buffer::int_plan): set after a p1v launch that limited the
+// block-internal edges of `plan` (nullptr clears); take returns that plan if it is still alive and
+// clears the marker
+void mark_internal(Buffer *adf_h, const Plan *plan);
+const Plan *take_internal(Buffer *adf_h);
+inline bool has_internal(const Buffer *adf_h) { return adf_h->int_plan != nullptr; }
 
 // ---- halo exchange (halo_rccl.hip): enqueue pack -> grouped ncclSend/ncclRecv -> unpack on the
 // halo plan's communication stream after the work already queued on `s`.  Returns an event that

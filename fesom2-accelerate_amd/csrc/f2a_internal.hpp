@@ -22,6 +22,10 @@ struct Buffer {
     hipEvent_t event = nullptr;
     bool has_event = false;
     uint64_t serial = 0;  // live-object serial (track_object): graph replays check it is unchanged
+    // fct_adf_h only: the mesh plan whose block-internal edges fct_ale_pre_comm_v_acc_ limited in
+    // p1v (fct_ale_post_comm_h_acc_ then limits the others; cleared by it and by every upload)
+    const void *int_plan = nullptr;
+    uint64_t int_serial = 0;
 };
 
 // One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the
@@ -88,15 +92,25 @@ struct MeshPlanDev {
     const NodeRec *node_rec = nullptr;    // [n_owned]
     const EdgeRef *p_edges = nullptr;     // node->edge CSR, processing order
     const RingRef *p_ring = nullptr;      // cluster CSR, processing order (if has ring)
-    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order,
-                                          // interior edges (both endpoints owned) first
+    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order:
+                                          // interior edges (both endpoints owned) first -- those
+                                          // crossing p1v blocks [0, n_ext_interior), then those
+                                          // inside one p1v block -- then the boundary edges
     int n_edge_interior = 0;
+    int n_ext_interior = 0;
     // packed b3h (variable depth): blocks of consecutive p_edge_info edges holding at most
     // kB3hPackSlots level pairs; b3p_desc[b] = {first edge, edges}, b3p_off[k] = slot offset of edge k
-    // in its block; descriptors [0, b3p_nint) cover the interior edges, the rest the boundary ones
+    // in its block; descriptors [0, b3p_next) cover the crossing interior edges, [b3p_next, b3p_nint)
+    // the block-internal ones, the rest the boundary edges
     const int2 *b3p_desc = nullptr;
     const unsigned short *b3p_off = nullptr;
-    int b3p_nint = 0, b3p_ndesc = 0, b3p_cap = 0;  // b3p_cap: level pairs per block
+    int b3p_next = 0, b3p_nint = 0, b3p_ndesc = 0, b3p_cap = 0;  // b3p_cap: level pairs per block
+    // b3-horizontal of the block-internal edges inside p1v (both endpoints' plus/minus are in the
+    // block's LDS after b2): for p1v block b (int_G positions of the processing order) the entries
+    // int_edges[int_ptr[b] .. int_ptr[b+1]) = {edge, column of edges(1,e), column of edges(2,e), lev}
+    int int_G = 0;                        // 0: no internal-edge lists
+    const int *int_ptr = nullptr;
+    const int4 *int_edges = nullptr;
     const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
     const int *p_owner_cum = nullptr;     // [n_owned + 1]: edges owned by processing positions < k
     // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of
@@ -150,6 +164,11 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 // phase 1 + the vertical half of phase 2 (b3v, cv need only the node's own column: no halo), then
 // phase 2's horizontal half alone (launch_p2h: c-horizontal; b3h stays its own kernel)
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
+// columns per p1v block for nl levels at vlimit 1 (the shape launch_p1v uses; the plan's int_G)
+int p1v_group_columns(int nl);
+// launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
+bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);
+constexpr int kMaxInternal = 64;  // most block-internal edges a p1v block limits (LDS staging)
 // opt-in phase-1 variants (fct_ale_variants.hip): *handled = false when no switch selects one
 hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool *handled);
 

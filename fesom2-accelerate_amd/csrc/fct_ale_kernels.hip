@@ -334,6 +334,29 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         if (VERT) a.del_v += tr * a.tr.node;
     }
     const int ncol = min(G, a.n_owned - first);
+    // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
+    // after b2, from the plus/minus in LDS.  Wave 0 stages their entries and slot offsets (one
+    // per lane, exclusive scan of ceil(lev/C)) while the records load.
+    int4 *ie_ent = reinterpret_cast<int4 *>(lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)));
+    int *ie_off = reinterpret_cast<int *>(ie_ent + kMaxInternal);  // [kMaxInternal + 1]: + total
+    if constexpr (VERT && (OPT & 16)) {
+        if (t < kWave) {
+            const int blk = first / G, i0 = mp.int_ptr[blk], n = mp.int_ptr[blk + 1] - i0;
+            const int4 ent = t < n ? mp.int_edges[i0 + t] : make_int4(0, 0, 0, 0);
+            const int sl = t < n ? (ent.w + C - 1) / C : 0;
+            int incl = sl;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const int v = __shfl_up(incl, d);
+                if (t >= d) incl += v;
+            }
+            if (t < kMaxInternal) {
+                ie_ent[t] = ent;
+                ie_off[t] = incl - sl;
+            }
+            if (t == kWave - 1) ie_off[kMaxInternal] = incl;
+        }
+    }
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     int j, u;
     slot_of(t, S, invS, j, u);
@@ -518,6 +541,31 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
         __syncthreads();
         const int top = Ln > 1 ? Ln : 1;                   // the Fortran always limits nz = 1
         const int na = col ? max(0, min(C, top - z0)) : 0;  // cells whose fct_adf_v is limited
+        if constexpr (OPT & 16) {
+            // b3-horizontal of the block-internal edges (docs/refactoring.md:237-263): every raw read
+            // of them (b1h of both endpoint columns) is behind the first barrier, no other block
+            // touches them, and both endpoints' final plus/minus are in LDS
+            const int total = ie_off[kMaxInternal];
+            for (int w = t; w < total; w += (int)blockDim.x) {
+                int lo_k = 0, hi_k = kMaxInternal - 1;  // last entry with ie_off <= w
+                while (lo_k < hi_k) {
+                    const int mid = (lo_k + hi_k + 1) >> 1;
+                    if (ie_off[mid] <= w) lo_k = mid;
+                    else hi_k = mid - 1;
+                }
+                const int4 e = ie_ent[lo_k];
+                const int zi = C * (w - ie_off[lo_k]);
+                const bool l1 = ODD && zi + 1 == L;
+                real f[C], out[C];
+                ldo<C, ODD>(a.adf_h + (size_t)e.x * L + zi, f, l1);
+                const int q1 = e.y * L + zi, q2 = e.z * L + zi;
+                const int nwi = min(C, e.w - zi);
+#pragma unroll
+                for (int c = 0; c < C; c++)
+                    out[c] = c < nwi ? b3h_factor(f[c], pl[q1 + c], mn[q1 + c], pl[q2 + c], mn[q2 + c]) * f[c] : 0.;
+                stv_s<C, true>(const_cast<real *>(a.adf_h) + (size_t)e.x * L + zi, out, nwi);
+            }
+        }
         if (na <= 0) return;
         if (nw == 0) {  // no wet cell (nlevels_nod2D <= 1): only nz = 1 is limited, from memory
             b = (size_t)ni.n * L + z0;
@@ -548,7 +596,7 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
 #pragma unroll
             for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
         } else if (nw > 0) {
-            real del_v[C], hn[C], hnn[C];
+            real del_v[C], hn[C], hnn[C], ar[C];
             if constexpr ((OPT & 8) && C == 2 && !ODD) {
                 const real *me = gl + C * threadIdx.x;
 #pragma unroll
@@ -562,7 +610,6 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
                 ldo_s<C, NT, ODD>(a.hnode + b, hn, last1);
                 ldo_s<C, NT, ODD>(a.hnode_new + b, hnn, last1);
             }
-            real ar[C];
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
             for (int c = 0; c < C; c++) {
@@ -1371,24 +1418,48 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     }
 }
 
+int p1v_group_columns(int nl)
+{
+    const int L = nl - 1;
+    if (odd_pairs(L)) return group_columns((L + 1) / 2);
+    return group_columns(L / levels_per_thread(L));
+}
+
+// the launch_p1v forms with the internal-edge tail: vlimit 1, the plan's block size, and the
+// default load placement (FESOM2_P1V_EARLY = 0)
+bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
+{
+    // (the opt-in phase-2 forms that limit every edge themselves keep all of them)
+    return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit == 1 && env_int("FESOM2_P1V_B3H", 1) != 0 &&
+           env_int("FESOM2_P1V_EARLY", 0) == 0 && !env_int("FESOM2_P2H_FUSE", 0) && !env_int("FESOM2_B3H_NODE", 0) &&
+           p1v_group_columns(a.nl) == mp.int_G;
+}
+
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const int L = a.nl - 1;
+    const bool in = p1v_limits_internal(mp, a);
+    const size_t lds_in = in ? kMaxInternal * sizeof(int4) + (kMaxInternal + 1) * sizeof(int) : 0;
     if (odd_pairs(L) && a.vlimit == 1) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec) + lds_in;
         if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
     }
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
-    const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
+    const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec) + lds_in;
     if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
     // OPT bits of k_p1 (VERT): 1 area_inv issued with the first loads, 2 + the tail's own streams
-    // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default)
+    // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default),
+    // 16 the block-internal edges' b3-horizontal (p1v_limits_internal)
     const int early = env_int("FESOM2_P1V_EARLY", 0) | (env_int("FESOM2_NL_PAIR", 1) ? 4 : 0);
+    if (in && C == 2 && early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
+    if (in && C == 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+    if (in) F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     if (C == 2) {
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1547,6 +1618,7 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
         int d0 = -1, d1 = -1;
         if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc;
         else if (begin == 0 && count == mp.n_edge_interior) d0 = 0, d1 = mp.b3p_nint;
+        else if (begin == 0 && count == mp.n_ext_interior) d0 = 0, d1 = mp.b3p_next;
         else if (begin == mp.n_edge_interior && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc;
         if (d0 >= 0) {
             const long groups = (long)(d1 - d0) * tr.n;

@@ -98,6 +98,7 @@ void transfer_var_(void **mem, real *host_ptr)
 {
     Buffer *b = buf(mem, "transfer_var_");
     if (!b) return;
+    mark_internal(b, nullptr);  // new raw contents
     b->host_pointer = host_ptr;
     h2d(b, true, nullptr, false);
 }
@@ -106,6 +107,7 @@ void transfer_var_async_(void **mem, real *host_ptr, void **stream, bool *record
 {
     Buffer *b = buf(mem, "transfer_var_async_");
     if (!b) return;
+    mark_internal(b, nullptr);
     b->host_pointer = host_ptr;
     h2d(b, false, stream_of(stream), record_event && *record_event);
 }
@@ -293,6 +295,7 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
         a.hnode_new = dptr<real>(bhn);
         a.del_v = dptr<real>(bdv);
         if (!run("fct_ale_p1v", st, [&] { return f2a::launch_p1v(plan->dev, a, st); })) return;
+        mark_internal(badfh, f2a::p1v_limits_internal(plan->dev, a) ? plan : nullptr);
         *alg_state = 7;
         if (!g_resident)
             for (Buffer *b : {bplus, bminus, badfv, bdv})
@@ -393,6 +396,11 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     const int ncols = (int)(std::min(bplus->size, bminus->size) / ((size_t)L * sizeof(real)));
     const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
     if (!plan) return;
+    if (has_internal(badfh)) {
+        report("fct_ale_post_comm_acc_: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by "
+               "fct_ale_post_comm_h_acc_");
+        return;
+    }
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
     // fused path: the production edge kernel over the plan's edge list (edge index order here)
     const bool stepwise = kernel_path() == 1;
@@ -493,6 +501,10 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
+    if (has_internal(badfh)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
+        report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
+        return;
+    }
     if (!g_resident && !comm && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
     hipEvent_t halo_done = nullptr;
     if (comm) {
@@ -642,6 +654,9 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
+    // the block-internal edges p1v limited already (fct_ale_pre_comm_v_acc_ marked fct_adf_h with
+    // its plan): b3h runs on the other edges of that plan's lists only
+    const Plan *ip = take_internal(badfh);
     if (!g_resident && !exch && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
     hipEvent_t halo_done = nullptr;
     if (exch) {
@@ -655,7 +670,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     // FESOM2_P2H_FUSE=1: b3-horizontal folded into the c-horizontal node kernel (k_p2hf, arrival
     // counters decide which endpoint stores the limited flux)
     const char *fz = getenv("FESOM2_P2H_FUSE");
-    if (fz && atoi(fz) != 0 && d.max_degree <= f2a::kMaxFusedDegree && (int)plan->owner_cum.size() == N + 1) {
+    if (!ip && fz && atoi(fz) != 0 && d.max_degree <= f2a::kMaxFusedDegree && (int)plan->owner_cum.size() == N + 1) {
         a.n_owned = N;
         const bool fresh = plan->cnt_tracers < ntr;
         a.edge_cnt = plan_edge_counters(plan, ntr);
@@ -684,11 +699,20 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     // FESOM2_B3H_NODE=1 (no exchange): b3h node-centric over the owner order -- exact, measured
     // 3-17 % slower than the edge-centric two-groups-per-block kernel
     const char *b3n = getenv("FESOM2_B3H_NODE");
-    const bool b3h_nodes = !exch && d.p_owner_cum && b3n && atoi(b3n) != 0;
+    const bool b3h_nodes = !ip && !exch && d.p_owner_cum && b3n && atoi(b3n) != 0;
+    const f2a::MeshPlanDev &de = ip ? ip->dev : d;  // the edge lists b3h runs on
+    const int eb = de.n_edge_interior;               // boundary edges (a halo endpoint): [eb, E)
     if (!run("fct_ale_b3_horizontal", st, [&] {
             if (b3h_nodes)
                 return f2a::launch_b3h_nodes(d, NL, plan->owner_cum.back(), E, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);
+            if (ip) {  // interior edges crossing p1v blocks; without an exchange the boundary ones too
+                const hipError_t e = f2a::launch_b3h_fused(de, NL, 0, de.n_ext_interior, dptr<real>(bplus),
+                                                           dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
+                if (e != hipSuccess || exch || eb >= E) return e;
+                return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
+                                             dptr<real>(badfh), a.tr, st);
+            }
             return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
                                          a.tr, st);
         }))
@@ -697,7 +721,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     if (exch) {
         if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
         if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
-                return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
+                return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);
             }))
             return;
@@ -810,6 +834,10 @@ static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_pl
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
+    if (has_internal(badfh)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
+        report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
+        return;
+    }
     if (!g_resident) {
         for (Buffer *b : {bplus, bminus, blo, badfv2, badfh2})
             if (!h2d(b, false, st, false)) return;
@@ -895,6 +923,38 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
     if (get_plan(mh, N, NT, E, *nl, true) && get_plan(mh, N, NT, E, *nl, false)) *istat = 0;
 }
 
+// Diagnostics of the mesh plan the phase-1 kernels run on (for the benchmark's byte counts):
+// info[0] p1v block columns of the internal-edge lists (0: none), [1] interior edges (both
+// endpoints owned), [2] interior edges crossing p1v blocks (b3h's), [3] block-internal edges
+// (limited inside p1v), [4] their edge cells (sum of levels).  *ninfo: entries written.
+void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
+                       int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                       void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                       void **nod2D_edges, void **elem2D_edges, long long *info, int *ninfo)
+{
+    *istat = 1;
+    (void)myDim_elem2D;
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D;
+    MeshHandles mh;
+    mh.edges = buf(nod2D_edges, "nod2D_edges");
+    mh.edge_tri = buf(elem2D_edges, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    mh.nlev_nod = buf(nlevels_nod2D, "nlevels_nod2D");
+    mh.elem_nodes = buf(elem2D_nodes, "elem2D_nodes");
+    mh.nie = buf(nod_in_elem2D, "nod_in_elem2D");
+    mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
+    mh.dim = *nod_in_elem2D_dim;
+    if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !mh.nlev_nod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
+    const Plan *plan = get_plan(mh, N, NT, E, *nl, true);
+    if (!plan) return;
+    const long long v[5] = {plan->dev.int_G, plan->dev.n_edge_interior, plan->dev.n_ext_interior,
+                            plan->dev.n_edge_interior - plan->dev.n_ext_interior, plan->int_cells};
+    const int n = std::min(*ninfo, 5);
+    for (int k = 0; k < n; k++) info[k] = v[k];
+    *ninfo = n;
+    *istat = 0;
+}
+
 void fesom2_download_(void **mem, void *host_ptr, int *istat)
 {
     Buffer *b = buf(mem, "fesom2_download_");
@@ -904,6 +964,7 @@ void fesom2_download_(void **mem, void *host_ptr, int *istat)
 void fesom2_upload_(void **mem, void *host_ptr, int *istat)
 {
     Buffer *b = buf(mem, "fesom2_upload_");
+    if (b) mark_internal(b, nullptr);  // new contents
     *istat = (b && ok(hipMemcpy(b->device_pointer, host_ptr, b->size, hipMemcpyHostToDevice), "H2D")) ? 0 : 1;
 }
 

@@ -53,6 +53,19 @@ class DeviceMesh:
                                    ip(m.dim), h["edges"].ref, h["edge_tri"].ref)
         check(st, "fesom2_prepare_mesh_")
 
+    def info(self):
+        """fesom2_mesh_info_: p1v block columns, interior edges, those crossing p1v blocks, the
+        block-internal ones (limited inside p1v) and their edge cells."""
+        m, h = self.m, self.h
+        st, n = C.c_int(0), C.c_int(5)
+        out = (C.c_longlong * 5)()
+        dll().fesom2_mesh_info_(C.byref(st), ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), h["nlev_nod"].ref,
+                                h["nlev_elem"].ref, h["elem2D_nodes"].ref, h["nie_num"].ref, h["nie"].ref,
+                                ip(m.dim), h["edges"].ref, h["edge_tri"].ref, out, C.byref(n))
+        check(st, "fesom2_mesh_info_")
+        keys = ("p1v_columns", "interior_edges", "crossing_edges", "internal_edges", "internal_edge_cells")
+        return dict(zip(keys, list(out)[: n.value]))
+
     def free(self):
         for h in self.h.values():
             if h:

@@ -137,6 +137,14 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
                           int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                           void **elem2D_nodes, void **nod_in_elem2D_num, void **nod_in_elem2D,
                           int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges);
+/* Diagnostics of the phase-1 mesh plan (built if needed): info[0] p1v block columns of the
+ * block-internal edge lists (0 = none), [1] interior edges, [2] interior edges crossing p1v blocks,
+ * [3] block-internal edges (limited inside fct_ale_pre_comm_v_acc_), [4] their edge cells.
+ * *ninfo: capacity in, entries written out. */
+void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
+                       int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
+                       void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
+                       void **nod2D_edges, void **elem2D_edges, long long *info, int *ninfo);
 /* Copy a handle's device contents to/from a host array (no rebinding), synchronous. */
 void fesom2_download_(void **mem, void *host_ptr, int *istat);
 void fesom2_upload_(void **mem, void *host_ptr, int *istat);

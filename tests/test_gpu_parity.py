@@ -437,7 +437,9 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_B3HP_H": "1"}, {"FESOM2_B3HP_H": "4"}, {"FESOM2_B3HP_CAP": "100"},
                {"FESOM2_P2H_FUSE": "1"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "1"},
                {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "4"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_NT": "0"},
-               {"FESOM2_P2H_FUSE": "1", "FESOM2_ODD_PAIR": "0"}]
+               {"FESOM2_P2H_FUSE": "1", "FESOM2_ODD_PAIR": "0"}, {"FESOM2_P1V_B3H": "0"},
+               {"FESOM2_P1V_B3H": "1", "FESOM2_SUBPATCH": "8"}, {"FESOM2_P1V_B3H": "1", "FESOM2_NL_PAIR": "0"},
+               {"FESOM2_P1V_B3H": "1", "FESOM2_CPT": "1"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3H_PACK": "0"}]
 
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
@@ -461,6 +463,38 @@ def test_fused_b3h_level_counts_and_repeats(nl, full, monkeypatch):
             check_pass(m, {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}, want)
     finally:
         e.free()
+        dm.free()
+
+
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_block_internal_edges(name, monkeypatch):
+    """p1v limits the block-internal edges (both endpoints among one p1v block's columns) and b3h the
+    rest: the plan reports them, the split pass stays exact, and a phase 2 other than
+    fct_ale_post_comm_h_acc_ after fct_ale_pre_comm_v_acc_ fails loudly instead of limiting twice."""
+    m, f = mesh(name)
+    dm = engine.DeviceMesh(m)
+    info = dm.info()
+    assert info["p1v_columns"] > 1 and 0 < info["internal_edges"] < info["interior_edges"] == m.E
+    assert info["crossing_edges"] + info["internal_edges"] == info["interior_edges"]
+    assert info["internal_edge_cells"] > info["internal_edges"]
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_c() != 9 and "fct_ale_post_comm_h_acc_" in abi.last_error()
+        for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(k)  # an upload clears the mark: the full fused pass runs again
+        assert e.full_pass() == 9, abi.last_error()
+        e.sync()
+        check_pass(m, {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")},
+                   O.full_pass(m, f))
+    finally:
+        e.free()
+        dm.free()
+    monkeypatch.setenv("FESOM2_P1V_B3H", "0")
+    dm = engine.DeviceMesh(m)
+    try:
+        assert dm.info()["internal_edges"] == 0
+    finally:
         dm.free()
 
 
