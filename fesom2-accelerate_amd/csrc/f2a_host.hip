@@ -615,6 +615,16 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         const int patch = env ? atoi(env) : (local_numbering ? 16384 : 4096);
         const char *senv = getenv("FESOM2_SUBPATCH");
         const int sub = senv ? atoi(senv) : 0;
+        // FESOM2_BLOB=1: cut each patch into compact blobs of one p1v block (greedy: the next node
+        // is the unassigned patch neighbour with the most edges into the blob), so more edges have
+        // both endpoints in one p1v block (limited there, see MeshPlanDev::int_ptr)
+        const char *benv = getenv("FESOM2_BLOB");
+        const int blob_g = (benv && atoi(benv) != 0) ? p1v_group_columns(nl) : 0;
+        std::vector<int> in_patch, bscore;
+        if (blob_g > 1) {
+            in_patch.assign(n_owned, -1);
+            bscore.assign(n_owned, 0);
+        }
         const char *oenv = getenv("FESOM2_PATCH_ORDER");
         const int porder = oenv ? atoi(oenv) : (local_numbering ? 0 : 1);
         std::vector<int> order;
@@ -675,6 +685,43 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     std::sort(cur.begin(), cur.end());
                 }
                 npatch++;
+                if (blob_g > 1 && (int)cur.size() > blob_g) {
+                    const int id = npatch;
+                    for (int v : cur) in_patch[v] = id;  // unassigned members of this patch
+                    std::vector<int> blob, cand;
+                    for (int v0 : cur) {  // seeds in the patch's order
+                        if (in_patch[v0] != id) continue;
+                        blob.assign(1, v0);
+                        in_patch[v0] = -2;
+                        cand.clear();
+                        auto touch = [&](int v) {
+                            for (int k = ptr[v]; k < ptr[v + 1]; k++) {
+                                const int w = other[k];
+                                if (w < n_owned && in_patch[w] == id) {
+                                    if (bscore[w]++ == 0) cand.push_back(w);
+                                }
+                            }
+                        };
+                        touch(v0);
+                        while ((int)blob.size() < blob_g && !cand.empty()) {
+                            size_t bi = 0;
+                            for (size_t q = 1; q < cand.size(); q++)
+                                if (bscore[cand[q]] > bscore[cand[bi]] ||
+                                    (bscore[cand[q]] == bscore[cand[bi]] && cand[q] < cand[bi]))
+                                    bi = q;
+                            const int w = cand[bi];
+                            cand.erase(cand.begin() + bi);
+                            bscore[w] = 0;
+                            in_patch[w] = -2;
+                            blob.push_back(w);
+                            touch(w);
+                        }
+                        for (int w : cand) bscore[w] = 0;
+                        std::sort(blob.begin(), blob.end());
+                        order.insert(order.end(), blob.begin(), blob.end());
+                    }
+                    continue;
+                }
                 if (sub > 1 && (int)cur.size() > sub) {
                     // FESOM2_SUBPATCH: cut the patch into compact BFS blobs of `sub` nodes (the
                     // fused kernels' columns per block), so a block's columns share their clusters
