@@ -172,7 +172,9 @@ def test_batched_partitioned_exchange(comm, overlap):
             assert np.array_equal(got, wants[k][name]), (name, k)
 
 
-def test_batched_split_by_direction():
+@pytest.mark.parametrize("internal", ["0", "1"])
+def test_batched_split_by_direction(internal, monkeypatch):
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)  # block-internal edges in p1v (per tracer) or not
     m = synth.config_mesh("8k x 20")
     tracers = synth.make_tracer_fields(m, 3)
     dm = engine.DeviceMesh(m)
@@ -188,9 +190,12 @@ def test_batched_split_by_direction():
         dm.free()
 
 
-def test_split_by_direction_partitioned_overlap(comm):
+@pytest.mark.parametrize("internal", ["0", "1"])
+def test_split_by_direction_partitioned_overlap(comm, internal, monkeypatch):
     """Two partitions, 2 tracers, the split entries with the exchange inside fct_ale_post_comm_h_acc_
-    (deranged halo repaired only by the one-rank exchange, as test_batched_partitioned_exchange)."""
+    (deranged halo repaired only by the one-rank exchange, as test_batched_partitioned_exchange);
+    with and without the block-internal edges limited in p1v."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)
     nx, ny, nl, ntr = 64, 48, 21, 2
     g = synth.make_mesh(nx, ny, nl)
     gtr = synth.make_tracer_fields(g, ntr)

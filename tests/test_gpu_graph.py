@@ -110,7 +110,8 @@ def test_replay_with_halo_exchange_two_tracers(comm, fuse, monkeypatch):
     """Two tracers of a partitioned mesh in ONE graph, each pre_comm_v -> post_comm_h(comm, plan) with
     the same halo plan (its stream and events reused twice in the capture).  Halo plus/minus are
     uploaded deranged before each replay; owned results must equal the single-domain oracle."""
-    monkeypatch.setenv("FESOM2_P2H_FUSE", fuse)  # b3h separate, or folded into c-horizontal
+    monkeypatch.setenv("FESOM2_P2H_FUSE", fuse)  # b3h folded into c-horizontal, or partly into p1v
+    monkeypatch.setenv("FESOM2_P1V_B3H", "0" if fuse == "1" else "1")
     nx, ny, nl, nranks, ntr = 64, 48, 21, 2, 2
     gm = synth.make_mesh(nx, ny, nl)
     gfields = synth.make_tracer_fields(gm, ntr)

@@ -445,10 +445,12 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
 @pytest.mark.parametrize("full", [False, True])
-def test_fused_b3h_level_counts_and_repeats(nl, full, monkeypatch):
-    """FESOM2_P2H_FUSE=1 (b3h folded into c-horizontal, arrival counters that are never reset): three
-    passes on the same plan, inputs re-uploaded before each, every one exact."""
-    monkeypatch.setenv("FESOM2_P2H_FUSE", "1")
+@pytest.mark.parametrize("mode", ["p2h_fuse", "p1v_internal"])
+def test_fused_b3h_level_counts_and_repeats(nl, full, mode, monkeypatch):
+    """FESOM2_P2H_FUSE=1 (b3h folded into c-horizontal, arrival counters that are never reset) and
+    FESOM2_P1V_B3H=1 (block-internal edges limited in p1v): three passes on the same plan, inputs
+    re-uploaded before each, every one exact."""
+    monkeypatch.setenv("FESOM2_P2H_FUSE" if mode == "p2h_fuse" else "FESOM2_P1V_B3H", "1")
     m = synth.make_mesh(40, 14, nl, full_depth=full)
     f = synth.make_fields(m)
     want = O.full_pass(m, f)
@@ -472,6 +474,7 @@ def test_block_internal_edges(name, monkeypatch):
     """p1v limits the block-internal edges (both endpoints among one p1v block's columns) and b3h the
     rest: the plan reports them, the split pass stays exact, and a phase 2 other than
     fct_ale_post_comm_h_acc_ after fct_ale_pre_comm_v_acc_ fails loudly instead of limiting twice."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", "1")  # (automatic from 32M wet cells)
     m, f = mesh(name)
     dm = engine.DeviceMesh(m)
     info = dm.info()
@@ -512,9 +515,12 @@ def test_split_variants_match_oracle(knobs, name, perm, monkeypatch):
 
 @pytest.mark.parametrize("name,full,perm", CASES + [("tiny", True, False)])
 @pytest.mark.parametrize("resident", [True, False])
-def test_split_by_direction_matches_oracle(name, full, perm, resident):
+@pytest.mark.parametrize("internal", ["0", "1"])
+def test_split_by_direction_matches_oracle(name, full, perm, resident, internal, monkeypatch):
     """fct_ale_pre_comm_v_acc_ (a1..b2 + b3v + cv) then fct_ale_post_comm_h_acc_ (b3h + ch): the
-    same results as the reference sequence, every output exact."""
+    same results as the reference sequence, every output exact (block-internal edges limited in p1v
+    or all in b3h)."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)
     m, f = mesh(name, full, perm)
     want = O.full_pass(m, f)
     abi.set_resident(resident)

@@ -41,11 +41,12 @@ MESHES = [(3000, 21, False), (20000, 48, False), (20000, 81, True), (500, 4, Fal
 
 
 @pytest.mark.parametrize("npts,nl,full", MESHES)
-@pytest.mark.parametrize("mode", ["split", "fused", "sequence", "stepwise"])
-def test_unstructured_paths_match_oracle(npts, nl, full, mode):
+@pytest.mark.parametrize("mode", ["split", "split_internal", "fused", "sequence", "stepwise"])
+def test_unstructured_paths_match_oracle(npts, nl, full, mode, monkeypatch):
     m, f = mesh(npts, nl, full)
     assert m.dim > 8  # some clusters overflow the inline NodeRec entries
-    if mode == "split":
+    monkeypatch.setenv("FESOM2_P1V_B3H", "1" if mode == "split_internal" else "0")
+    if mode.startswith("split"):
         got = run_split(m, f)
     else:
         st, got = run_pass(m, f, fused=mode == "fused", path="stepwise" if mode == "stepwise" else "fused")
