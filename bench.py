@@ -137,6 +137,23 @@ def cpu_all_cores(args, budget=4.0):
                       f"{min(r[2] for r in res)} passes ({slowest:.3f} s/pass)"}
 
 
+def stream_ceiling(args):
+    """The chip's streaming rates measured on this GPU right now (tools/stream_probe.hip, a child
+    process): a flat 16-B copy, and p1v's own 11-read/4-write stream pattern in its block shape
+    without gathers or arithmetic.  None when the probe is not built or fails."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "stream_probe")
+    if not os.path.exists(exe):
+        return None
+    nx, ny, nl = synth.CONFIGS[args.config]
+    try:
+        out = subprocess.run([exe, str(nx * ny), str(nl - 1), "--json"], capture_output=True, text=True,
+                             timeout=120, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, OSError, ValueError, IndexError):
+        return None
+
+
 def host_info():
     model = ""
     try:
@@ -283,6 +300,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_all = cpu_all_cores(args)
         log(f"cpu all cores: {cpu_all}")
+
+    ceiling = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ceiling = stream_ceiling(args)  # own process, before this one touches the GPU
+        log(f"stream ceiling: {ceiling}")
 
     abi.dll()  # engine first: one HIP runtime for the process
     abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
@@ -492,6 +514,11 @@ def main():
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s", "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic,
                 "alg_bytes_per_launch": kb[dom], "avg_launch_ms": round(avg_s * 1e3, 4)}
+        if ceiling:  # context: what this GPU streams (copy) and streams in p1v's pattern, same run
+            roof["stream_ceiling"] = dict(ceiling, frac_of_copy=round(achieved / ceiling["copy_GBps"], 4),
+                                          tool="tools/stream_probe.hip")
+            if dom == "fct_ale_p1v" and args.tracers == 1:
+                roof["stream_ceiling"]["frac_of_p1v_pattern"] = round(achieved / ceiling["p1v_pattern_GBps"], 4)
     pass_gbs = kb["survey_pass"] / (ms_step * 1e-3) / 1e9
 
     # ---- CPU baseline (rank 0, N = 1 only)

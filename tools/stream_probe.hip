@@ -7,12 +7,14 @@
 //   flat   13 reads + 4 writes per level pair, thread = pair, linear order
 //   cols   the same in p1v's block shape: G = 8 columns x L/2 threads, XCD-swizzled tiles, the three
 //          stride-nl arrays at nl = L+1 (8-byte aligned 16-B loads), adf_h as three columns per node
-// Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe tools/stream_probe.hip
-// Run:   ./stream_probe [nodes=1200000] [L=80]
+// Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe tools/stream_probe.hip (build() does)
+// Run:   ./stream_probe [nodes=1200000] [L=80] [--json]   (--json: one line with the copy and the
+//        G = 8 column-pattern rates, which bench.py reports beside the roofline)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef double d2 __attribute__((ext_vector_type(2), aligned(8)));
@@ -84,6 +86,8 @@ int main(int argc, char **argv)
 {
     const long nodes = argc > 1 ? atol(argv[1]) : 1200000;
     const int L = argc > 2 ? atoi(argv[2]) : 80;
+    const bool json = argc > 3 && std::string(argv[3]) == "--json";
+    double copy_tbs = 0, cols_tbs = 0;
     const long cn = nodes * L, cnl = nodes * (L + 1);
     std::vector<double *> bufs;
     auto alloc = [&](long n) {
@@ -123,25 +127,33 @@ int main(int argc, char **argv)
         float ms = 0;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("%-28s %8.3f ms  %7.1f GB  %6.2f TB/s\n", name, ms, bytes / 1e9, bytes / (ms * 1e-3) / 1e12);
+        const double tbs = bytes / (ms * 1e-3) / 1e12;
+        if (!json) printf("%-28s %8.3f ms  %7.1f GB  %6.2f TB/s\n", name, ms, bytes / 1e9, tbs);
         fflush(stdout);
+        return tbs;
     };
     const long n2 = 2 * cn;  // d2 elements of the copy
-    timeit("copy (16 B/lane)", 2.0 * 16 * n2, [&] {
+    copy_tbs = timeit("copy (16 B/lane)", 2.0 * 16 * n2, [&] {
         hipLaunchKernelGGL(k_copy, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, 0, (const d2 *)src, (d2 *)dst, n2);
     });
     const long np = cn / 2;
-    timeit("flat 11R+4W", bytes_p1, [&] {
-        hipLaunchKernelGGL(k_flat, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, 0, a, np);
-    });
+    if (!json)
+        timeit("flat 11R+4W", bytes_p1, [&] {
+            hipLaunchKernelGGL(k_flat, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, 0, a, np);
+        });
     for (int G : {4, 8, 16, 24}) {
+        if (json && G != 8) continue;
         char nm[64];
         snprintf(nm, sizeof nm, "cols G=%d 11R+4W", G);
         const int thr = ((G * (L / 2) + 63) / 64) * 64;
-        timeit(nm, bytes_p1, [&] {
+        const double r = timeit(nm, bytes_p1, [&] {
             hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G);
         });
+        if (G == 8) cols_tbs = r;
     }
+    if (json)
+        printf("{\"copy_GBps\": %.1f, \"p1v_pattern_GBps\": %.1f, \"nodes\": %ld, \"levels\": %d}\n", copy_tbs * 1e3,
+               cols_tbs * 1e3, nodes, L);
     for (double *p : bufs) CHECK(hipFree(p));
     return 0;
 }
