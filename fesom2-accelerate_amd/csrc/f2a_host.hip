@@ -1073,13 +1073,12 @@ void mark_internal(Buffer *adf_h, const Plan *plan)
     adf_h->int_serial = plan ? plan->serial : 0;
 }
 
-const Plan *take_internal(Buffer *adf_h)
+const Plan *peek_internal(const Buffer *adf_h)
 {
     const void *p = adf_h->int_plan;
-    const uint64_t serial = adf_h->int_serial;
-    adf_h->int_plan = nullptr;
-    return p && object_live(p, serial) ? static_cast<const Plan *>(p) : nullptr;
+    return p && object_live(p, adf_h->int_serial) ? static_cast<const Plan *>(p) : nullptr;
 }
+
 
 void drop_plans_of(const Buffer *b)
 {

@@ -161,11 +161,11 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                      bool with_ring);
 void drop_plans_of(const Buffer *b);
 // fct_adf_h's internal-edge marker (Buffer::int_plan): set after a p1v launch that limited the
-// block-internal edges of `plan` (nullptr clears); take returns that plan if it is still alive and
-// clears the marker
+// block-internal edges of `plan` (nullptr clears)
 void mark_internal(Buffer *adf_h, const Plan *plan);
-const Plan *take_internal(Buffer *adf_h);
 inline bool has_internal(const Buffer *adf_h) { return adf_h->int_plan != nullptr; }
+// the marked plan if it is still alive (the mark stays)
+const Plan *peek_internal(const Buffer *adf_h);
 
 // ---- halo exchange (halo_rccl.hip): enqueue pack -> grouped ncclSend/ncclRecv -> unpack on the
 // halo plan's communication stream after the work already queued on `s`.  Returns an event that

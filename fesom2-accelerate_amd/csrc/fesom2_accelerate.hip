@@ -655,8 +655,13 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
     // the block-internal edges p1v limited already (fct_ale_pre_comm_v_acc_ marked fct_adf_h with
-    // its plan): b3h runs on the other edges of that plan's lists only
-    const Plan *ip = take_internal(badfh);
+    // its plan): b3h runs on the other edges of that plan's lists only; the mark is cleared once
+    // the whole phase has been enqueued
+    const Plan *ip = peek_internal(badfh);
+    if (has_internal(badfh) && !ip) {
+        report("fct_ale_post_comm_h_acc_: the mesh plan fct_ale_pre_comm_v_acc_ limited fct_adf_h with was freed");
+        return;
+    }
     if (!g_resident && !exch && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
     hipEvent_t halo_done = nullptr;
     if (exch) {
@@ -692,6 +697,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
                                              dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
             }))
             return;
+        mark_internal(badfh, nullptr);
         *alg_state = 9;
         if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
         return;
@@ -729,6 +735,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
         a.count = N - n_first;
         if (!run("fct_ale_p2h_boundary", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
     }
+    mark_internal(badfh, nullptr);
     *alg_state = 9;
     if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
 }
