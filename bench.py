@@ -191,8 +191,9 @@ def build_local(args, rank, world):
 def verify(args, e, step, m, fields, rank, world, dist):
     """One pass on the pristine inputs, owned results gathered on rank 0 and compared cell for cell
     with the oracle's single-domain pass over the global mesh (every tracer)."""
-    for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
-        e.upload(name)  # the host arrays were never touched in resident mode
+    for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h", "adf_v2", "adf_h2"):
+        if name in e.host:
+            e.upload(name)  # the host arrays were never touched in resident mode (adf_*2: zeros)
     step()
     abi.device_sync()
     L, ntr = m.L, len(fields)
@@ -226,7 +227,7 @@ def verify(args, e, step, m, fields, rank, world, dist):
     wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
     bad = {}
     for k, fk in enumerate(synth.make_tracer_fields(g, ntr)):
-        want = O.full_pass(g, fk)
+        want = O.iterated_pass(g, fk, args.fct_iter) if args.fct_iter > 1 else O.full_pass(g, fk, vlimit=args.vlimit)
         for p in parts:
             gid = npos[p["gid"]]
             for name in ("plus", "minus"):
@@ -275,6 +276,11 @@ def main():
                     help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
                          "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
                          "sequence; a PCIe-inclusive rate for DESIGN.md, not the benchmark value (1 GPU, 1 tracer)")
+    ap.add_argument("--vlimit", type=int, default=1, choices=[1, 2, 3],
+                    help="vertical limiter of a3 (docs/refactoring.md:113-148; reference.cpp has 1 only)")
+    ap.add_argument("--fct-iter", type=int, default=1,
+                    help="FESOM2's iterative FCT (iter_yn, SURVEY.md 8(f) 1): a step is K-1 rounds of "
+                         "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final fused pass; 1 GPU")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
                          "oracle on the global mesh (gathered over ranks)")
@@ -353,7 +359,10 @@ def main():
     dm.prepare()
     mi = dm.info()
     mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
-    e = engine.FctAle(dm, f, copy=False) if args.tracers == 1 else engine.FctAleBatch(dm, fields)
+    if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or args.transfers):
+        raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
+    e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
+        engine.FctAleBatch(dm, fields, vlimit=args.vlimit)
     stream = e.stream
 
     halo = None
@@ -401,6 +410,11 @@ def main():
     def step():
         if args.transfers:
             return step_transfers()
+        if args.fct_iter > 1:  # iter_yn: K-1 rounds of phase 1 + iterative phase 2, then the final pass
+            s_it = e.iterated_pass(args.fct_iter)
+            if s_it != 9:
+                raise RuntimeError(f"iterated pass alg_state {s_it}: {abi.last_error()}")
+            return
         if args.path == "split":
             s1 = e.pre_comm_v()
             if s1 != 7:
@@ -488,7 +502,7 @@ def main():
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
     s = mesh_stats(m)
     s.update(mesh_info)
-    kb = kernel_bytes(s, args.tracers, split=args.path == "split")
+    kb = kernel_bytes(s, args.tracers, split=args.path == "split" and args.fct_iter == 1)
     per_kernel = {}
     for name, (cnt, tot) in stats.items():
         avg = tot / max(cnt, 1)
@@ -556,7 +570,7 @@ def main():
                                    + (" per GPU" if args.scaling == "weak" else f" split over {world} GPU(s)")
                                    + f", {args.tracers} tracer{'s' if args.tracers > 1 else ''}"
                                    + (" (batched)" if args.tracers > 1 else ""),
-                       "tracers": args.tracers,
+                       "tracers": args.tracers, "vlimit": args.vlimit, "fct_iterations": args.fct_iter,
                        "nodes_per_gpu": m.N, "levels": m.L,
                        "global_nodes": global_dims(args, world)[0] * global_dims(args, world)[1],
                        "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],

@@ -404,23 +404,23 @@ namespace f2a {
 
 // ----------------------------------------------------------------------------- plans
 
-// Packed b3h blocks (MeshPlanDev::b3p_*): greedy over the edge list, separately for the ranges
-// [0, n_ext), [n_ext, n_int) and [n_int, E) so the exchange-overlap split and the p1v-internal edges
-// keep their own descriptors.
-static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_ext, int n_int)
+// Packed b3h blocks: greedy over an edge list, separately for each range [bounds[i], bounds[i+1])
+// (the exchange-overlap split keeps its interior / boundary descriptors); ends[i] = descriptors of
+// ranges < i+1.  Returns false only if an edge cannot fit a block (unreachable, see cap).
+static bool pack_edges(const std::vector<int4> &einfo, const std::vector<int> &bounds, int &cap,
+                       std::vector<int2> &desc, std::vector<unsigned short> &off, std::vector<int> &ends)
 {
-    std::vector<int2> desc;
-    std::vector<unsigned short> off(einfo.size());
-    int ends[3] = {0, 0, 0};
+    desc.clear();
+    ends.clear();
+    off.assign(einfo.size(), 0);
     const char *cenv = getenv("FESOM2_B3HP_CAP");  // level pairs per block (A/B; default kB3hPackSlots)
     // at least one edge of the deepest kind per block (else no block could take it), and at most
     // 2048 pairs = a 1024-thread block at two slots per thread (the launch falls back to two slots
     // per thread whenever one slot per thread would need more than 1024 threads)
     int lmax = 0;
     for (const int4 &ei : einfo) lmax = std::max(lmax, ei.z);
-    const int cap = std::max({64, (lmax + 1) / 2, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048)});
-    const int bounds[4] = {0, n_ext, n_int, (int)einfo.size()};
-    for (int part = 0; part < 3; part++) {
+    cap = std::max({64, (lmax + 1) / 2, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048)});
+    for (size_t part = 0; part + 1 < bounds.size(); part++) {
         int k = bounds[part];
         const int k_end = bounds[part + 1];
         while (k < k_end) {
@@ -436,13 +436,22 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
             if (k == k0) return false;  // unreachable with cap >= ceil(lmax / 2); never loop forever
             desc.push_back(make_int2(k0, k - k0));
         }
-        ends[part] = (int)desc.size();
+        ends.push_back((int)desc.size());
     }
+    return true;
+}
+
+// MeshPlanDev::b3p_* over p_edge_info: descriptors [0, b3p_nint) for the interior edges, the rest
+// for the boundary ones
+static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_int)
+{
+    std::vector<int2> desc;
+    std::vector<unsigned short> off;
+    std::vector<int> ends;
+    if (!pack_edges(einfo, {0, n_int, (int)einfo.size()}, d.b3p_cap, desc, off, ends)) return false;
     d.b3p_desc = plan->mem.upload(desc);
     d.b3p_off = plan->mem.upload(off);
-    d.b3p_next = ends[0];
-    d.b3p_nint = ends[1];
-    d.b3p_cap = cap;
+    d.b3p_nint = ends[0];
     d.b3p_ndesc = (int)desc.size();
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }
@@ -878,32 +887,48 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             std::vector<int> pos(n_owned);
             for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
             auto internal = [&](const int4 &ei) { return pos[ei.x] / IG == pos[ei.y] / IG; };
-            const auto mid = std::stable_partition(einfo.begin(), einfo.begin() + d.n_edge_interior,
-                                                   [&](const int4 &ei) { return !internal(ei); });
-            d.n_ext_interior = (int)(mid - einfo.begin());
+            // the interior edges crossing p1v blocks, in processing order (b3h's list on the split
+            // path; p_edge_info keeps every edge in processing order for the other paths)
+            std::vector<int4> ext;
             const int nblk = (n_owned + IG - 1) / IG;
             std::vector<int> iptr(nblk + 1, 0);
-            std::vector<int4> iedges;
-            for (int k = d.n_ext_interior; k < d.n_edge_interior; k++) iptr[pos[einfo[k].x] / IG + 1]++;
+            for (int k = 0; k < d.n_edge_interior; k++) {
+                if (internal(einfo[k])) iptr[pos[einfo[k].x] / IG + 1]++;
+                else ext.push_back(einfo[k]);
+            }
             int most = 0;
             for (int b = 0; b < nblk; b++) {
                 most = std::max(most, iptr[b + 1]);
                 iptr[b + 1] += iptr[b];
             }
-            iedges.resize(iptr[nblk]);
+            std::vector<int4> iedges(iptr[nblk]);
             std::vector<int> fill(iptr.begin(), iptr.end() - 1);
-            for (int k = d.n_ext_interior; k < d.n_edge_interior; k++) {
+            for (int k = 0; k < d.n_edge_interior; k++) {
                 const int4 ei = einfo[k];
+                if (!internal(ei)) continue;
                 const int b = pos[ei.x] / IG;
                 // {edge, column of edges(1,e), column of edges(2,e), lev}: einfo keeps edges(1/2,e) order
                 iedges[fill[b]++] = make_int4(ei.w, pos[ei.x] - b * IG, pos[ei.y] - b * IG, ei.z);
             }
             if (most <= kMaxInternal && nblk > 0 && !iedges.empty()) {
+                std::vector<int2> xdesc;
+                std::vector<unsigned short> xoff;
+                std::vector<int> xends;
+                int xcap = 0;
+                if (!pack_edges(ext, {0, (int)ext.size()}, xcap, xdesc, xoff, xends))
+                    return fail("packing the crossing edges failed");
                 d.int_G = IG;
                 for (const int4 &ie : iedges) plan->int_cells += ie.w;
                 d.int_ptr = plan->mem.upload(iptr);
                 d.int_edges = plan->mem.upload(iedges);
-                if (!d.int_ptr || !d.int_edges) return fail("device allocation for the internal edge lists failed");
+                d.n_ext_interior = (int)ext.size();
+                d.p_edge_ext = plan->mem.upload(ext);
+                d.b3x_desc = plan->mem.upload(xdesc);
+                d.b3x_off = plan->mem.upload(xoff);
+                d.b3x_ndesc = (int)xdesc.size();
+                d.b3x_cap = xcap;
+                if (!d.int_ptr || !d.int_edges || (!ext.empty() && (!d.p_edge_ext || !d.b3x_desc || !d.b3x_off)))
+                    return fail("device allocation for the internal edge lists failed");
             } else {  // nothing to gain, or a block with too many: every interior edge crosses
                 d.n_ext_interior = d.n_edge_interior;
             }
@@ -975,7 +1000,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         d.p_ring = with_ring ? plan->mem.upload(pring) : nullptr;
         d.p_edge_info = plan->mem.upload(einfo);
         if (!d.node_info || !d.node_rec || !d.p2_rec || !d.p_edges || (with_ring && !d.p_ring) || !d.p_edge_info ||
-            !build_b3h_pack(plan.get(), d, einfo, d.n_ext_interior, d.n_edge_interior))
+            !build_b3h_pack(plan.get(), d, einfo, d.n_edge_interior))
             return fail("device allocation for the processing order failed");
     } else if (n_edges > 0) {
         std::vector<int4> einfo(n_edges);
@@ -983,7 +1008,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             einfo[e] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
         d.n_edge_interior = d.n_ext_interior = n_edges;
         d.p_edge_info = plan->mem.upload(einfo);
-        if (!d.p_edge_info || !build_b3h_pack(plan.get(), d, einfo, n_edges, n_edges))
+        if (!d.p_edge_info || !build_b3h_pack(plan.get(), d, einfo, n_edges))
             return fail("device allocation for the edge list failed");
     }
     return plan;

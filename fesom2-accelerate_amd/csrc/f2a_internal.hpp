@@ -92,19 +92,22 @@ struct MeshPlanDev {
     const NodeRec *node_rec = nullptr;    // [n_owned]
     const EdgeRef *p_edges = nullptr;     // node->edge CSR, processing order
     const RingRef *p_ring = nullptr;      // cluster CSR, processing order (if has ring)
-    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order:
-                                          // interior edges (both endpoints owned) first -- those
-                                          // crossing p1v blocks [0, n_ext_interior), then those
-                                          // inside one p1v block -- then the boundary edges
+    const int4 *p_edge_info = nullptr;    // [n_edges] {node1, node2, lev, edge}, processing order,
+                                          // interior edges (both endpoints owned) first
     int n_edge_interior = 0;
-    int n_ext_interior = 0;
     // packed b3h (variable depth): blocks of consecutive p_edge_info edges holding at most
     // kB3hPackSlots level pairs; b3p_desc[b] = {first edge, edges}, b3p_off[k] = slot offset of edge k
-    // in its block; descriptors [0, b3p_next) cover the crossing interior edges, [b3p_next, b3p_nint)
-    // the block-internal ones, the rest the boundary edges
+    // in its block; descriptors [0, b3p_nint) cover the interior edges, the rest the boundary ones
     const int2 *b3p_desc = nullptr;
     const unsigned short *b3p_off = nullptr;
-    int b3p_next = 0, b3p_nint = 0, b3p_ndesc = 0, b3p_cap = 0;  // b3p_cap: level pairs per block
+    int b3p_nint = 0, b3p_ndesc = 0, b3p_cap = 0;  // b3p_cap: level pairs per block
+    // the interior edges crossing p1v blocks (b3h's list on the split path when p1v limits the
+    // block-internal ones), processing order, packed the same way
+    int n_ext_interior = 0;
+    const int4 *p_edge_ext = nullptr;
+    const int2 *b3x_desc = nullptr;
+    const unsigned short *b3x_off = nullptr;
+    int b3x_ndesc = 0, b3x_cap = 0;
     // b3-horizontal of the block-internal edges inside p1v (both endpoints' plus/minus are in the
     // block's LDS after b2): for p1v block b (int_G positions of the processing order) the entries
     // int_edges[int_ptr[b] .. int_ptr[b+1]) = {edge, column of edges(1,e), column of edges(2,e), lev}
@@ -202,6 +205,9 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
+// b3-horizontal over the interior edges crossing p1v blocks (mp.p_edge_ext)
+hipError_t launch_b3h_ext(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
+                          const Tracers &tr, hipStream_t s);
 // chunk c's node kernel and the next chunk's b3h in one launch (node blocks first; one tracer)
 hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int4 *einfo, int n_edges, hipStream_t s);
 // the same over an explicit edge list

@@ -1425,14 +1425,22 @@ int p1v_group_columns(int nl)
     return group_columns(L / levels_per_thread(L));
 }
 
+// columns per block of launch_p1v's shape for this vlimit (odd L in level pairs at vlimit 1 only)
+static int p1v_launch_G(int nl, int vlimit)
+{
+    const int L = nl - 1;
+    if (vlimit == 1) return p1v_group_columns(nl);
+    return group_columns(L / levels_per_thread(L));
+}
+
 // the launch_p1v forms with the internal-edge tail: vlimit 1, the plan's block size, and the
 // default load placement (FESOM2_P1V_EARLY = 0)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 {
     // (the opt-in phase-2 forms that limit every edge themselves keep all of them)
-    return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit == 1 && env_int("FESOM2_P1V_B3H", 1) != 0 &&
-           env_int("FESOM2_P1V_EARLY", 0) == 0 && !env_int("FESOM2_P2H_FUSE", 0) && !env_int("FESOM2_B3H_NODE", 0) &&
-           p1v_group_columns(a.nl) == mp.int_G;
+    return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit >= 1 && a.vlimit <= 3 &&
+           env_int("FESOM2_P1V_B3H", 1) != 0 && env_int("FESOM2_P1V_EARLY", 0) == 0 && !env_int("FESOM2_P2H_FUSE", 0) &&
+           !env_int("FESOM2_B3H_NODE", 0) && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
 }
 
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
@@ -1457,6 +1465,14 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default),
     // 16 the block-internal edges' b3-horizontal (p1v_limits_internal)
     const int early = env_int("FESOM2_P1V_EARLY", 0) | (env_int("FESOM2_NL_PAIR", 1) ? 4 : 0);
+    if (in && a.vlimit == 2) {
+        if (C == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (in && a.vlimit == 3) {
+        if (C == 2) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+    }
     if (in && C == 2 && early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     if (in) F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1609,51 +1625,62 @@ hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int 
     return launch_b3h_edges(mp.p_edge_owner + owned_edges, n_edges - owned_edges, nl, plus, minus, adf_h, tr, s);
 }
 
+// packed b3h over descriptors [d0, d1) of a list (k_b3h_p), or false if packing is off for this L
+static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const int4 *einfo, int cap, int d0, int d1,
+                              int nl, const real *plus, const real *minus, real *adf_h, const Tracers &tr,
+                              hipStream_t s, hipError_t *err)
+{
+    const int L = nl - 1;
+    if (!desc || !env_int("FESOM2_B3H_PACK", 1) || !(L % 2 == 0 || odd_pairs(L))) return false;
+    const long groups = (long)(d1 - d0) * tr.n;
+    const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
+    init_swizzle();
+    *err = hipSuccess;
+    if (groups <= 0) return true;
+    // slots per thread; the 1- and 4-slot forms exist for even L with non-temporal streams only,
+    // and the block must cover the capacity for the form actually launched
+    int H = env_int("FESOM2_B3HP_H", 2);
+    if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
+    const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
+    if (H == 1)
+        hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+    else if (H == 4)
+        hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+    else if (L % 2)
+        hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+    else if (NT)
+        hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+    else
+        hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+    *err = hipGetLastError();
+    return true;
+}
+
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
     // packed by depth (FESOM2_B3H_PACK=1): the plan's descriptors for exactly these edge ranges
-    const int L = nl - 1;
-    if (mp.b3p_desc && env_int("FESOM2_B3H_PACK", 1) && (L % 2 == 0 || odd_pairs(L))) {
-        int d0 = -1, d1 = -1;
-        if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc;
-        else if (begin == 0 && count == mp.n_edge_interior) d0 = 0, d1 = mp.b3p_nint;
-        else if (begin == 0 && count == mp.n_ext_interior) d0 = 0, d1 = mp.b3p_next;
-        else if (begin == mp.n_edge_interior && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc;
-        if (d0 >= 0) {
-            const long groups = (long)(d1 - d0) * tr.n;
-            const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
-            init_swizzle();
-            if (groups <= 0) return hipSuccess;
-            // slots per thread; the 1- and 4-slot forms exist for even L with non-temporal streams only,
-            // and the block must cover the capacity for the form actually launched
-            int H = env_int("FESOM2_B3HP_H", 2);
-            if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && mp.b3p_cap > 1024)) H = 2;
-            const dim3 grid((unsigned)groups), block((mp.b3p_cap + H - 1) / H);
-            if (H == 1) {
-                hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
-                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
-                return hipGetLastError();
-            }
-            if (H == 4) {
-                hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
-                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
-                return hipGetLastError();
-            }
-            if (L % 2) {
-                hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off, mp.p_edge_info,
-                                   L, plus, minus, adf_h, tr);
-            } else if (NT) {
-                hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
-                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
-            } else {
-                hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, mp.b3p_desc + d0, mp.b3p_off,
-                                   mp.p_edge_info, L, plus, minus, adf_h, tr);
-            }
-            return hipGetLastError();
-        }
-    }
+    int d0 = -1, d1 = -1;
+    if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc;
+    else if (begin == 0 && count == mp.n_edge_interior) d0 = 0, d1 = mp.b3p_nint;
+    else if (begin == mp.n_edge_interior && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc;
+    hipError_t err;
+    if (d0 >= 0 && launch_b3h_packed(mp.b3p_desc, mp.b3p_off, mp.p_edge_info, mp.b3p_cap, d0, d1, nl, plus, minus,
+                                     adf_h, tr, s, &err))
+        return err;
     return launch_b3h_edges(mp.p_edge_info + begin, count, nl, plus, minus, adf_h, tr, s);
+}
+
+hipError_t launch_b3h_ext(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
+                          const Tracers &tr, hipStream_t s)
+{
+    if (mp.n_ext_interior == 0) return hipSuccess;
+    if (!mp.p_edge_ext) return hipErrorInvalidValue;
+    hipError_t err;
+    if (launch_b3h_packed(mp.b3x_desc, mp.b3x_off, mp.p_edge_ext, mp.b3x_cap, 0, mp.b3x_ndesc, nl, plus, minus, adf_h,
+                          tr, s, &err))
+        return err;
+    return launch_b3h_edges(mp.p_edge_ext, mp.n_ext_interior, nl, plus, minus, adf_h, tr, s);
 }
 
 hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus, const real *minus,

@@ -713,8 +713,8 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
                 return f2a::launch_b3h_nodes(d, NL, plan->owner_cum.back(), E, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);
             if (ip) {  // interior edges crossing p1v blocks; without an exchange the boundary ones too
-                const hipError_t e = f2a::launch_b3h_fused(de, NL, 0, de.n_ext_interior, dptr<real>(bplus),
-                                                           dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
+                const hipError_t e =
+                    f2a::launch_b3h_ext(de, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
                 if (e != hipSuccess || exch || eb >= E) return e;
                 return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);

@@ -539,8 +539,12 @@ def test_split_by_direction_matches_oracle(name, full, perm, resident, internal,
 
 
 @pytest.mark.parametrize("vlimit", [2, 3])
-def test_split_by_direction_vlimit(vlimit):
-    m, f = mesh("8k x 20")
+@pytest.mark.parametrize("name,internal", [("8k x 20", "0"), ("8k x 20", "1"), ("127k x 47", "1")])
+def test_split_by_direction_vlimit(vlimit, name, internal, monkeypatch):
+    """vlimit 2/3 on the split path, with and without the block-internal edges limited in p1v (odd L:
+    the vlimit-2/3 shape has other blocks than the plan's lists, so p1v leaves them to b3h)."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)
+    m, f = mesh(name)
     st, p1 = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
     want = O.post_comm(m, f, p1["plus"], p1["minus"])
     dm = engine.DeviceMesh(m)
