@@ -99,9 +99,14 @@ def kernel_bytes(s, ntr=1, split=False):
     # c-horizontal with b3h folded in: raw adf_h read, limited adf_h written once, plus/minus of both
     # endpoints (owned + halo columns), del_h rw; area shared
     p2hf = ntr * 8 * (2 * cn + 2 * ce + 2 * (cn + ch)) + 8 * cn + 4 * N + ints_edges + 4 * E
+    # reference entry sequence on the fused kernels: b3v alone (plus/minus, adf_v rw) and the c-step
+    # node kernel (cv + ch: del_v, del_h rw; ttf, LO, adf_v, adf_h; area, hnode, hnode_new shared)
+    b3v = ntr * 8 * (2 * cn + 2 * cn1) + 4 * N
+    c_step = ntr * 8 * (4 * cn + 2 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
             "fct_ale_p1v": p1v, "fct_ale_p2h": p2h, "fct_ale_p2h_b3h": p2hf,
+            "fct_ale_b3_vertical": b3v, "fct_ale_c": c_step,
             "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 
