@@ -1377,7 +1377,7 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
 {
     const float invS = 1.0f / (float)S;
     const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real) + (size_t)G * sizeof(NodeRec);
-    const bool NT = (env_int("FESOM2_NT", 2) & 1) != 0;
+    const bool NT = (env_int("FESOM2_NT", 6) & 1) != 0;
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (NT) F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1453,8 +1453,13 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec) + lds_in;
         if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
-        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
-        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
+        const float inv = 1.0f / (float)S;
+        if ((env_int("FESOM2_NT", 6) & 4) != 0) {  // non-temporal single-use streams (see below)
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
     }
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
@@ -1473,6 +1478,11 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (C == 2) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     }
+    // FESOM2_NT bit 2: p1v's single-use streams non-temporal (plus/minus/del_v stores, the tail's
+    // del_v/hnode/hnode_new loads; measured -1.5 % per pass; the stride-nl ones stay cached: +1 %)
+    const bool nt = (env_int("FESOM2_NT", 6) & 4) != 0;
+    if (in && C == 2 && early == 4 && nt)
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2 && early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     if (in) F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1480,6 +1490,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 1) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 1>), groups, G, S, lds, s, mp, a, G, invS);
+        if (early == 4 && nt) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 5) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 5>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 12) {
@@ -1502,7 +1513,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
         const long groups = (long)(a.count + G - 1) / G * a.tr.n;
         const size_t lds = (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
-        if ((env_int("FESOM2_NT", 2) & 2) != 0)
+        if ((env_int("FESOM2_NT", 6) & 2) != 0)
             F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
@@ -1510,7 +1521,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
-    const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;
+    const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;
     const bool pair = env_int("FESOM2_NL_PAIR", 1) != 0;  // 16-B loads of the stride-nl area (ld_nl)
     if (C == 2) {
         if (NT && pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1530,7 +1541,7 @@ hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec) + G * sizeof(unsigned);
-    const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;
+    const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;
     const int KB = env_int("FESOM2_P2HF_KB", 2);
     if (odd) {
         if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1556,12 +1567,12 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     const int KB = env_int("FESOM2_P2_BATCH", 4);
     const size_t lds = (size_t)G * sizeof(NodeRec);
     if (C == 2) {
-        const bool NT = (env_int("FESOM2_NT", 2) & 2) != 0;  // measured: p2 streams non-temporal (-2 %)
+        const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;  // measured: p2 streams non-temporal (-2 %)
         if (NT) F2A_LAUNCH_GROUPS((k_p2<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if ((env_int("FESOM2_NT", 2) & 2) != 0) F2A_LAUNCH_GROUPS((k_p2<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+    if ((env_int("FESOM2_NT", 6) & 2) != 0) F2A_LAUNCH_GROUPS((k_p2<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
     if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
