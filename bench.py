@@ -178,12 +178,17 @@ def global_dims(args, world):
     return (nx, ny * world, nl) if args.scaling == "weak" else (nx, ny, nl)
 
 
+def delaunay(args, npts, nl):
+    return synth.delaunay_mesh(npts, nl, full_depth=not args.parity_levels,
+                               numbering="hilbert" if args.mesh == "delaunay-hilbert" else "scipy")
+
+
 def build_local(args, rank, world):
     nx, ny, nl = global_dims(args, world)
-    if args.mesh == "delaunay":
+    if args.mesh != "structured":
         if world > 1:
-            raise SystemExit("--mesh delaunay is a single-GPU variant")
-        return synth.delaunay_mesh(nx * ny, nl, full_depth=not args.parity_levels), None
+            raise SystemExit("--mesh delaunay* is a single-GPU variant")
+        return delaunay(args, nx * ny, nl), None
     g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels, name=f"{args.config} x {world}")
     if world == 1:
         return (synth.permute_mesh(g) if args.permuted else g), None
@@ -221,7 +226,7 @@ def verify(args, e, step, m, fields, rank, world, dist):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     nx, ny, nl = global_dims(args, world)
-    g = synth.delaunay_mesh(nx * ny, nl, full_depth=not args.parity_levels) if args.mesh == "delaunay" else \
+    g = delaunay(args, nx * ny, nl) if args.mesh != "structured" else \
         synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels)
     if args.permuted:  # the oracle runs on the same numbering (sums follow the local edge order)
         g = synth.permute_mesh(g)
@@ -261,9 +266,10 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: the config per GPU; strong: the config split over the GPUs (SURVEY.md 8(e))")
     ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
-    ap.add_argument("--mesh", default="structured", choices=["structured", "delaunay"],
+    ap.add_argument("--mesh", default="structured", choices=["structured", "delaunay", "delaunay-hilbert"],
                     help="delaunay: Delaunay triangulation of as many random points as the config has nodes "
-                         "(degrees 3..13, scattered numbering; 1 GPU)")
+                         "(degrees 3..13, scattered numbering; 1 GPU); delaunay-hilbert: the same points "
+                         "numbered along a Hilbert curve (the locality of a renumbered FESOM2 mesh)")
     ap.add_argument("--permuted", action="store_true",
                     help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -571,7 +577,8 @@ def main():
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
             "config": {"workload": f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}"
-                                   + (" Delaunay mesh" if args.mesh == "delaunay" else "")
+                                   + {"structured": "", "delaunay": " Delaunay mesh",
+                                      "delaunay-hilbert": " Delaunay mesh, Hilbert numbering"}[args.mesh]
                                    + (" per GPU" if args.scaling == "weak" else f" split over {world} GPU(s)")
                                    + f", {args.tracers} tracer{'s' if args.tracers > 1 else ''}"
                                    + (" (batched)" if args.tracers > 1 else ""),

@@ -110,18 +110,52 @@ def make_mesh(nx, ny, nl, seed=42, full_depth=False, name=""):
                 edge_gid=np.arange(E, dtype=np.int64), name=name or f"{nx}x{ny}x{nl - 1}")
 
 
-def delaunay_mesh(npts, nl, seed=11, full_depth=False, name=""):
+def hilbert_key(xy, bits=16):
+    """Index along a Hilbert curve of order ``bits`` of points in the unit square (vectorised xy2d)."""
+    n = 1 << bits
+    x = np.minimum((xy[:, 0] * n).astype(np.int64), n - 1)
+    y = np.minimum((xy[:, 1] * n).astype(np.int64), n - 1)
+    d = np.zeros(len(xy), np.int64)
+    s = n >> 1
+    while s > 0:
+        rx = ((x & s) > 0).astype(np.int64)
+        ry = ((y & s) > 0).astype(np.int64)
+        d += s * s * ((3 * rx) ^ ry)
+        # rotate the quadrant so the sub-curve has the canonical orientation
+        flip = (ry == 0) & (rx == 1)
+        x = np.where(flip, n - 1 - x, x)
+        y = np.where(flip, n - 1 - y, y)
+        swap = ry == 0
+        x, y = np.where(swap, y, x), np.where(swap, x, y)
+        s >>= 1
+    return d
+
+
+def delaunay_mesh(npts, nl, seed=11, full_depth=False, name="", numbering="scipy"):
     """Unstructured variant: the Delaunay triangulation of ``npts`` random points in the unit square.
 
     Node degrees vary (3 .. ~12, unlike the structured mesh's 6), so clusters and edge lists overflow
-    the 8 inline NodeRec entries; the numbering is scipy's (scattered).  Same array conventions as
-    :func:`make_mesh` (1-based, ``edge_tri`` second entry 0 on the boundary, element levels uniform in
-    [3, nl] unless ``full_depth``, node levels = max over the adjacent elements).
+    the 8 inline NodeRec entries.  Same array conventions as :func:`make_mesh` (1-based, ``edge_tri``
+    second entry 0 on the boundary, element levels uniform in [3, nl] unless ``full_depth``, node
+    levels = max over the adjacent elements).
+
+    ``numbering="scipy"``: the points' random order (scattered numbering, the plan's Cuthill-McKee case).
+    ``numbering="hilbert"``: nodes numbered along a Hilbert curve and elements by the curve index of their
+    centroid -- the locality a FESOM2 mesh has after its partitioner's renumbering (same triangulation,
+    same edges set).
     """
     from scipy.spatial import Delaunay
 
     rng = np.random.default_rng(seed)
-    tri = Delaunay(rng.random((npts, 2))).simplices.astype(np.int64)  # (T, 3), 0-based
+    pts = rng.random((npts, 2))
+    tri = Delaunay(pts).simplices.astype(np.int64)  # (T, 3), 0-based
+    if numbering == "hilbert":
+        new = np.empty(npts, np.int64)
+        new[np.argsort(hilbert_key(pts), kind="stable")] = np.arange(npts)
+        tri = new[tri]
+        tri = tri[np.argsort(hilbert_key(pts[np.argsort(new)][tri].mean(axis=1)), kind="stable")]
+    elif numbering != "scipy":
+        raise ValueError(f"delaunay_mesh: unknown numbering {numbering!r}")
     T = len(tri)
     e = np.concatenate([tri[:, [0, 1]], tri[:, [1, 2]], tri[:, [2, 0]]])
     e.sort(axis=1)
@@ -151,7 +185,7 @@ def delaunay_mesh(npts, nl, seed=11, full_depth=False, name=""):
     return Mesh(nl=nl, N=npts, H=0, T=T, E=E, dim=dim, elem2D_nodes=i32(tri + 1), edges=i32(edges + 1),
                 edge_tri=i32(et), nie_num=i32(deg), nie=i32(nie), nlev_elem=i32(le), nlev_nod=i32(ln),
                 node_gid=np.arange(npts, dtype=np.int64), edge_gid=np.arange(E, dtype=np.int64),
-                name=name or f"delaunay{npts}x{nl - 1}")
+                name=name or f"delaunay{npts}x{nl - 1}" + ("+hilbert" if numbering == "hilbert" else ""))
 
 
 def config_mesh(name, full_depth=False, seed=42):

@@ -20,10 +20,10 @@ pytestmark = pytest.mark.gpu
 _CACHE = {}
 
 
-def mesh(npts, nl, full):
-    key = (npts, nl, full)
+def mesh(npts, nl, full, numbering="scipy"):
+    key = (npts, nl, full, numbering)
     if key not in _CACHE:
-        m = synth.delaunay_mesh(npts, nl, full_depth=full)
+        m = synth.delaunay_mesh(npts, nl, full_depth=full, numbering=numbering)
         _CACHE[key] = (m, synth.make_fields(m))
     return _CACHE[key]
 
@@ -40,10 +40,13 @@ def device():
 MESHES = [(3000, 21, False), (20000, 48, False), (20000, 81, True), (500, 4, False)]
 
 
-@pytest.mark.parametrize("npts,nl,full", MESHES)
+@pytest.mark.parametrize("npts,nl,full,numbering", [k + ("scipy",) for k in MESHES] +
+                         [(30000, 48, False, "hilbert"), (20000, 81, True, "hilbert")])
 @pytest.mark.parametrize("mode", ["split", "split_internal", "fused", "sequence", "stepwise"])
-def test_unstructured_paths_match_oracle(npts, nl, full, mode, monkeypatch):
-    m, f = mesh(npts, nl, full)
+def test_unstructured_paths_match_oracle(npts, nl, full, numbering, mode, monkeypatch):
+    """numbering "hilbert": the plan takes the sorted-patch order (locality detected), "scipy": the
+    Cuthill-McKee patches."""
+    m, f = mesh(npts, nl, full, numbering)
     assert m.dim > 8  # some clusters overflow the inline NodeRec entries
     monkeypatch.setenv("FESOM2_P1V_B3H", "1" if mode == "split_internal" else "0")
     if mode.startswith("split"):

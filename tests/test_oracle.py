@@ -74,10 +74,12 @@ def test_oracle_matches_reference_cpp(name, full, perm):
 
 
 @pytest.mark.skipif(O.ref() is None, reason="oracle/_ref (reference.cpp build) not present")
-@pytest.mark.parametrize("npts,nl,full", [(3000, 21, False), (2000, 48, True), (5000, 12, False)])
-def test_oracle_matches_reference_cpp_unstructured(npts, nl, full):
-    """Delaunay meshes: node degrees 3..13 and scattered numbering (the structured meshes have 6)."""
-    m = synth.delaunay_mesh(npts, nl, full_depth=full)
+@pytest.mark.parametrize("npts,nl,full,numbering", [(3000, 21, False, "scipy"), (2000, 48, True, "scipy"),
+                                                    (5000, 12, False, "scipy"), (4000, 21, False, "hilbert")])
+def test_oracle_matches_reference_cpp_unstructured(npts, nl, full, numbering):
+    """Delaunay meshes: node degrees 3..13 and scattered (or Hilbert-curve) numbering (the structured
+    meshes have degree 6)."""
+    m = synth.delaunay_mesh(npts, nl, full_depth=full, numbering=numbering)
     assert m.dim > 8
     f = synth.make_fields(m)
     st, got = O.pre_comm(m, f)
@@ -85,6 +87,25 @@ def test_oracle_matches_reference_cpp_unstructured(npts, nl, full):
     want = O.ref_pre_comm(m, f)
     for k in ("ttf_max", "ttf_min", "plus", "minus", "UV"):
         assert np.array_equal(got[k].view(np.uint64), want[k].view(np.uint64)), k
+
+
+def test_hilbert_numbering_is_a_renumbering():
+    """synth.delaunay_mesh(numbering="hilbert") is the same triangulation with nodes along a Hilbert
+    curve: same element/edge counts and degree histogram, edges between nearby numbers."""
+    a = synth.delaunay_mesh(3000, 11)
+    b = synth.delaunay_mesh(3000, 11, numbering="hilbert")
+    assert (a.N, a.T, a.E, a.dim) == (b.N, b.T, b.E, b.dim)
+    assert np.array_equal(np.sort(a.nie_num), np.sort(b.nie_num))
+    e = b.edges.reshape(-1, 2).astype(np.int64)
+    assert np.median(np.abs(e[:, 0] - e[:, 1])) < 16 < np.median(np.abs(np.diff(a.edges.reshape(-1, 2), axis=1)))
+    # every element's nodes are its nod_in_elem2D entries' owners
+    en = b.elem2D_nodes.reshape(-1, 3) - 1
+    nie = b.nie.reshape(b.N, b.dim)
+    for n in range(0, b.N, 97):
+        els = nie[n, : b.nie_num[n]] - 1
+        assert np.all(np.any(en[els] == n, axis=1))
+    k = synth.hilbert_key(np.array([[(i + .5) / 4, (j + .5) / 4] for i in range(4) for j in range(4)]), bits=2)
+    assert sorted(k) == list(range(16))
 
 
 def test_vlimit_protocol_of_reference_cpp():
