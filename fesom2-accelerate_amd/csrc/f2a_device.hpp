@@ -248,6 +248,31 @@ __device__ __forceinline__ void ldo(const real *__restrict__ p, real (&v)[C], bo
         ldv<C>(p, v);
     }
 }
+// The same with the pointer already moved one level back for the last slot (p = column + z0 - last1):
+// no per-load address select
+template <int C, bool ODD>
+__device__ __forceinline__ void ldo_pre(const real *__restrict__ p, real (&v)[C], bool last1)
+{
+    if constexpr (ODD && C == 2) {
+        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(p);
+        v[0] = last1 ? t.y : t.x;
+        v[1] = last1 ? 0. : t.y;
+    } else {
+        ldv<C>(p, v);
+    }
+}
+template <int C, bool NT, bool ODD>
+__device__ __forceinline__ void ldo_s_pre(const real *__restrict__ p, real (&v)[C], bool last1)
+{
+    if constexpr (ODD && C == 2) {
+        const f2a_d2u *q = reinterpret_cast<const f2a_d2u *>(p);
+        const f2a_d2u t = NT ? __builtin_nontemporal_load(q) : *q;
+        v[0] = last1 ? t.y : t.x;
+        v[1] = last1 ? 0. : t.y;
+    } else {
+        ldv_s<C, NT>(p, v);
+    }
+}
 template <int C, bool NT, bool ODD>
 __device__ __forceinline__ void ldo_s(const real *__restrict__ p, real (&v)[C], bool last1)
 {
@@ -301,21 +326,22 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
                                               const real *__restrict__ ttf, int z0, int L,
                                               real (&vx)[C], real (&vn)[C], bool last1 = false)
 {
+    const int zl = (ODD && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
     for (int r = r0; r < r1; r += kBatch) {
         size_t idx[kBatch];
         int lev[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             const RingRef rr = (r + k < r1) ? ring[r + k] : RingRef{0, 0};
-            idx[k] = (size_t)rr.node * L + z0;
+            idx[k] = (size_t)rr.node * L + zl;
             lev[k] = rr.lev;
         }
         real lo[kBatch][C], tt[kBatch][C];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             if (z0 < lev[k]) {
-                ldo<C, ODD>(LO + idx[k], lo[k], last1);
-                ldo<C, ODD>(ttf + idx[k], tt[k], last1);
+                ldo_pre<C, ODD>(LO + idx[k], lo[k], last1);
+                ldo_pre<C, ODD>(ttf + idx[k], tt[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) lo[k][c] = tt[k][c] = 0.;
@@ -347,13 +373,14 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
                                           const real *__restrict__ adf_h, int z0, int L, F &&f,
                                           bool last1 = false)
 {
+    const int zl = (ODD && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
         size_t idx[kBatch];
         int code[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             const EdgeRef er = (k0 + k < e1) ? edges[k0 + k] : EdgeRef{0, 0, 0};
-            idx[k] = (size_t)er.edge * L + z0;
+            idx[k] = (size_t)er.edge * L + zl;
             code[k] = er.code;
         }
         real h[kBatch][C];
@@ -363,7 +390,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
                 if constexpr (COH)
                     ldv_coh<C>(adf_h + idx[k], h[k]);
                 else
-                    ldo<C, ODD>(adf_h + idx[k], h[k], last1);
+                    ldo_pre<C, ODD>(adf_h + idx[k], h[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // (every raw fct_adf_v read of the block happened before the first one), and del_ttf_advvert is
 // updated -- the arithmetic of k_p2, so results are identical.
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
-__global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
+__device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
     const int L = a.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
@@ -420,8 +420,9 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
-        ldo<C, ODD>(a.LO + b, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
-        ldo<C, ODD>(a.ttf + b, tt, last1);
+        const size_t bl = b - ((ODD && last1) ? 1 : 0);  // odd L: the last slot's pair starts a level early
+        ldo_pre<C, ODD>(a.LO + bl, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
+        ldo_pre<C, ODD>(a.ttf + bl, tt, last1);
         if constexpr (OPT & 1) {
             // OPT & 1: the own-column streams of b2 and the vertical tail are issued with the first
             // loads, so they land during the gathers instead of after the barriers
@@ -606,9 +607,10 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
                     hnn[c] = me[2 * gl_n + c];
                 }
             } else {
-                ldo_s<C, NT, ODD>(a.del_v + b, del_v, last1);
-                ldo_s<C, NT, ODD>(a.hnode + b, hn, last1);
-                ldo_s<C, NT, ODD>(a.hnode_new + b, hnn, last1);
+                const size_t bl = b - ((ODD && last1) ? 1 : 0);
+                ldo_s_pre<C, NT, ODD>(a.del_v + bl, del_v, last1);
+                ldo_s_pre<C, NT, ODD>(a.hnode + bl, hn, last1);
+                ldo_s_pre<C, NT, ODD>(a.hnode_new + bl, hnn, last1);
             }
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
@@ -632,6 +634,12 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
             }
         if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
     }
+}
+
+template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
+__global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
+{
+    p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
 
 // Phase 2, horizontal half (after the exchange, with b3h): c-horizontal only (see k_p1 VERT).
