@@ -291,7 +291,8 @@ def main():
                     help="vertical limiter of a3 (docs/refactoring.md:113-148; reference.cpp has 1 only)")
     ap.add_argument("--fct-iter", type=int, default=1,
                     help="FESOM2's iterative FCT (iter_yn, SURVEY.md 8(f) 1): a step is K-1 rounds of "
-                         "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final fused pass; 1 GPU")
+                         "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final pass (--path "
+                         "split: the direction-split entries, fused: pre_comm -> post_comm_c); 1 GPU")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
                          "oracle on the global mesh (gathered over ranks)")
@@ -422,7 +423,7 @@ def main():
         if args.transfers:
             return step_transfers()
         if args.fct_iter > 1:  # iter_yn: K-1 rounds of phase 1 + iterative phase 2, then the final pass
-            s_it = e.iterated_pass(args.fct_iter)
+            s_it = e.iterated_pass(args.fct_iter, final="split" if args.path == "split" else "fused")
             if s_it != 9:
                 raise RuntimeError(f"iterated pass alg_state {s_it}: {abi.last_error()}")
             return
@@ -513,7 +514,7 @@ def main():
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
     s = mesh_stats(m)
     s.update(mesh_info)
-    kb = kernel_bytes(s, args.tracers, split=args.path == "split" and args.fct_iter == 1)
+    kb = kernel_bytes(s, args.tracers, split=args.path == "split")
     per_kernel = {}
     for name, (cnt, tot) in stats.items():
         avg = tot / max(cnt, 1)

@@ -1152,25 +1152,22 @@ __global__ __launch_bounds__(1024) void k_p2_iter(MeshPlanDev mp, P2IterArgs a, 
                 // LO + (adf_v(nz) - adf_v(nz+1)) * dt / area / hnode_new, left to right
                 if (c < nw) lo[c] = lo[c] + (lim[c] - lim[c + 1]) * a.dt / ar[c] / hnn[c];
             }
-            const int ne = ni.e1 - ni.e0;
-            for (int k = 0; k < ne; k++) {  // ascending edge order, as the Fortran edge loop
-                const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
-                const int lev = er.code >> 1, second = er.code & 1;
-                if (z0 >= lev) continue;
-                const int other = a.edges[2 * er.edge + (second ? 0 : 1)] - 1;
-                real h[C], po[C], mo[C];
-                ldv<C>(a.adf_h + (size_t)er.edge * L + z0, h);
-                ldv<C>(a.plus + (size_t)other * L + z0, po);
-                ldv<C>(a.minus + (size_t)other * L + z0, mo);
+            // the node's edges in ascending edge order (the Fortran edge loop's addition order), two
+            // edges' raw flux and other-endpoint plus/minus in flight at a time, limited in-thread
+            real pn[C], mn[C];
 #pragma unroll
-                for (int c = 0; c < C; c++) {
-                    if (z0 + c >= lev) continue;
-                    const real ae = second ? b3h_factor(h[c], po[c], mo[c], pp[c + 1], mm[c + 1])
-                                           : b3h_factor(h[c], pp[c + 1], mm[c + 1], po[c], mo[c]);
-                    const real lh = ae * h[c];
-                    lo[c] = second ? lo[c] - lh * a.dt / ar[c] / hnn[c] : lo[c] + lh * a.dt / ar[c] / hnn[c];
-                }
+            for (int c = 0; c < C; c++) {
+                pn[c] = pp[c + 1];
+                mn[c] = mm[c + 1];
             }
+            auto add = [&](int c, real lh, int second, int) {
+                lo[c] = second ? lo[c] - lh * a.dt / ar[c] / hnn[c] : lo[c] + lh * a.dt / ar[c] / hnn[c];
+            };
+            const int ne = ni.e1 - ni.e0;
+            for_edges_limited<C, 1>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L, add);
+            if (ne > kRecEdge)
+                for_edges_limited<C, 1>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                        add);
         }
     }
     __syncthreads();  // every raw fct_adf_v read of the block precedes the writes
@@ -1211,8 +1208,9 @@ __global__ __launch_bounds__(1024) void k_b3h_iter(const int4 *__restrict__ einf
     const size_t i = (size_t)ei.w * L + z0;
     const size_t i1 = (size_t)ei.x * L + z0, i2 = (size_t)ei.y * L + z0;
     real f[C], h2[C], p1[C], m1[C], p2[C], m2[C];
-    ldv<C>(adf_h + i, f);
-    ldv<C>(adf_h2 + i, h2);
+    ldv_s<C, true>(adf_h + i, f);  // single-use streams: non-temporal
+    // fct_adf_h2 keeps its old value (and fct_adf_h takes it) only on the levels below the edge's
+    if (z0 + C > ei.z) ldv_s<C, true>(adf_h2 + i, h2);
     if (z0 < ei.z) {
         ldv<C>(plus + i1, p1);
         ldv<C>(minus + i1, m1);
@@ -1222,8 +1220,8 @@ __global__ __launch_bounds__(1024) void k_b3h_iter(const int4 *__restrict__ einf
 #pragma unroll
     for (int c = 0; c < C; c++)
         if (z0 + c < ei.z) h2[c] = (1.0 - b3h_factor(f[c], p1[c], m1[c], p2[c], m2[c])) * f[c];
-    stv<C>(adf_h2 + i, h2, C);
-    stv<C>(adf_h + i, h2, C);
+    stv_s<C, true>(adf_h2 + i, h2, C);
+    stv_s<C, true>(adf_h + i, h2, C);
 }
 
 // columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads)

@@ -210,8 +210,11 @@ class FctAle:
             dp(self.dt))
         return st.value
 
-    def iterated_pass(self, iterations):
-        """``iterations - 1`` iter_yn rounds then the final fused pass (final alg_state)."""
+    def iterated_pass(self, iterations, final="split"):
+        """``iterations - 1`` iter_yn rounds then the final pass (final alg_state): the
+        direction-split entries (``final="split"``, the fastest) or the fused pre_comm -> post_comm_c
+        pair (``"fused"``).  The rounds hand over the LO update and the remainder fluxes only, so the
+        final pass is an ordinary one on them."""
         for _ in range(iterations - 1):
             s1 = self.pre_comm()
             if s1 != 6:
@@ -219,7 +222,7 @@ class FctAle:
             s2 = self.post_comm_iter()
             if s2 != 9:
                 return s2
-        return self.full_pass()
+        return self.split_pass() if final == "split" else self.full_pass()
 
     def exchange(self, comm, plan):
         """fct_ale_exchange_acc_: RCCL halo exchange of fct_plus/fct_minus on this stream."""

@@ -309,17 +309,19 @@ def test_reference_named_entries_run_on_gpu():
 @pytest.mark.parametrize("name", ["tiny", "8k x 20", "127k x 47"])
 @pytest.mark.parametrize("iterations", [2, 3])
 @pytest.mark.parametrize("resident", [True, False])
-def test_iter_yn_iterations_match_oracle(name, iterations, resident):
+@pytest.mark.parametrize("final", ["split", "fused"])
+def test_iter_yn_iterations_match_oracle(name, iterations, resident, final):
     """iter_yn (docs/refactoring.md:227-290): iterations-1 rounds of fct_ale_post_comm_iter_acc_
-    (LO update + remainder hand-over) then the final pass; every array equals the oracle's
-    restatement of the Fortran (parity unpinned: no executable reference holds this branch)."""
+    (LO update + remainder hand-over) then the final pass (direction-split or fused entries); every
+    array equals the oracle's restatement of the Fortran (parity unpinned: no executable reference
+    holds this branch)."""
     m, f = mesh(name)
     want = O.iterated_pass(m, f, iterations)
     abi.set_resident(resident)
     dm = engine.DeviceMesh(m)
     e = engine.FctAle(dm, f)
     try:
-        assert e.iterated_pass(iterations) == 9, abi.last_error()
+        assert e.iterated_pass(iterations, final=final) == 9, abi.last_error()
         e.sync()
         got = {k: e.download(k) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h", "LO", "adf_v2",
                                           "adf_h2")}
@@ -339,7 +341,7 @@ def test_iter_yn_batched():
     dm = engine.DeviceMesh(m)
     e = engine.FctAleBatch(dm, tracers)
     try:
-        assert e.iterated_pass(2) == 9, abi.last_error()
+        assert e.iterated_pass(2) == 9, abi.last_error()  # final pass: the batched split entries
         e.sync()
         for k in range(3):
             want = O.iterated_pass(m, tracers[k], 2)
