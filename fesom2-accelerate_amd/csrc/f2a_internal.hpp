@@ -172,6 +172,18 @@ int p1v_group_columns(int nl);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);
 constexpr int kMaxInternal = 64;  // most block-internal edges a p1v block limits (LDS staging)
+// LDS of that staging (int4 entries + int slot offsets), rounded to whole doubles
+__host__ __device__ constexpr size_t p1_internal_lds_bytes()
+{
+    return (kMaxInternal * sizeof(int4) + (kMaxInternal + 1) * sizeof(int) + 7) / 8 * 8;
+}
+// dynamic LDS of a phase-1 block (k_p1): tvert max/min, the G NodeRecs, the internal-edge staging,
+// and for vlimit 2/3 the own columns' max(LO, ttf)
+inline size_t p1_lds_bytes(int G, int L, int vlimit, bool internal)
+{
+    return (2 + (vlimit != 1 ? 1 : 0)) * (size_t)G * L * sizeof(double) + (size_t)G * 192 +
+           (internal ? p1_internal_lds_bytes() : 0);
+}
 // opt-in phase-1 variants (fct_ale_variants.hip): *handled = false when no switch selects one
 hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool *handled);
 

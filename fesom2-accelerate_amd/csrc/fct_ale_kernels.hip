@@ -357,6 +357,10 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             if (t == kWave - 1) ie_off[kMaxInternal] = incl;
         }
     }
+    // VLIMIT 2/3: max(LO, ttf) of the own column, for the 3-point vertical bound after the barrier
+    // (behind the records and the internal-edge staging: p1_lds_bytes)
+    real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
+                ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     int j, u;
     slot_of(t, S, invS, j, u);
@@ -472,6 +476,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             if (!ODD || c == 0 || !last1) {  // ODD: the last slot's second level is the next column's
                 tvx[q + c] = vx[c];
                 tvn[q + c] = vn[c];
+                if (VLIMIT != 1) cmx[q + c] = RMAX(lo[c], tt[c]);  // read on wet levels only
             }
     }
     __syncthreads();
@@ -503,11 +508,10 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
         } else {
             tm = tvx[q + c];
             tn = tvn[q + c];
-            if (z >= 1 && z < Ln - 1) {
-                const size_t bz = b + c;
-                const real c0 = RMAX(a.LO[bz - 1], a.ttf[bz - 1]);
-                const real c1 = RMAX(a.LO[bz], a.ttf[bz]);
-                const real c2 = RMAX(a.LO[bz + 1], a.ttf[bz + 1]);
+            if (z >= 1 && z < Ln - 1) {  // levels z-1 .. z+1 of the own column, from LDS
+                const real c0 = cmx[q + c - 1];
+                const real c1 = cmx[q + c];
+                const real c2 = cmx[q + c + 1];
                 const real hmx = RMAX(RMAX(c0, c1), c2);
                 const real hmn = RMIN(RMIN(c0, c1), c2);  // Fortran :121/:141 as written
                 if (VLIMIT == 2) {
@@ -1382,7 +1386,7 @@ template <int C, int RB, int EB>
 static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, int G, int S, long groups)
 {
     const float invS = 1.0f / (float)S;
-    const size_t lds = 2 * (size_t)G * (a.nl - 1) * sizeof(real) + (size_t)G * sizeof(NodeRec);
+    const size_t lds = p1_lds_bytes(G, a.nl - 1, a.vlimit, false);
     const bool NT = (env_int("FESOM2_NT", 6) & 1) != 0;
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1453,11 +1457,10 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const int L = a.nl - 1;
     const bool in = p1v_limits_internal(mp, a);
-    const size_t lds_in = in ? kMaxInternal * sizeof(int4) + (kMaxInternal + 1) * sizeof(int) : 0;
     if (odd_pairs(L) && a.vlimit == 1) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-        const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec) + lds_in;
+        const size_t lds = p1_lds_bytes(G, L, 1, in);
         if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
         const float inv = 1.0f / (float)S;
         if ((env_int("FESOM2_NT", 6) & 4) != 0) {  // non-temporal single-use streams (see below)
@@ -1470,12 +1473,21 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
-    const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec) + lds_in;
+    const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
     if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
     // OPT bits of k_p1 (VERT): 1 area_inv issued with the first loads, 2 + the tail's own streams
     // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default),
     // 16 the block-internal edges' b3-horizontal (p1v_limits_internal)
     const int early = env_int("FESOM2_P1V_EARLY", 0) | (env_int("FESOM2_NL_PAIR", 1) ? 4 : 0);
+    // FESOM2_NT bit 2: p1v's single-use streams non-temporal (plus/minus/del_v stores, the tail's
+    // del_v/hnode/hnode_new loads; measured -1.5 % per pass; the stride-nl ones stay cached: +1 %)
+    const bool nt = (env_int("FESOM2_NT", 6) & 4) != 0;
+    if (a.vlimit != 1 && C == 2 && early == 4 && nt) {  // vlimit 2/3 in the production shape
+        if (in && a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
+        if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
+        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+    }
     if (in && a.vlimit == 2) {
         if (C == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1484,9 +1496,6 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (C == 2) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    // FESOM2_NT bit 2: p1v's single-use streams non-temporal (plus/minus/del_v stores, the tail's
-    // del_v/hnode/hnode_new loads; measured -1.5 % per pass; the stride-nl ones stay cached: +1 %)
-    const bool nt = (env_int("FESOM2_NT", 6) & 4) != 0;
     if (in && C == 2 && early == 4 && nt)
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2 && early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
