@@ -525,14 +525,18 @@ def main():
         per_kernel[name] = entry
     dom = max(stats, key=lambda k: stats[k][1]) if stats else None
     traffic = None
-    try:
-        with open(args.traffic) as fh:
-            tr = json.load(fh)
+    slug = args.config.replace(" ", "").replace(".", "p")  # "127k x 47" -> profiles/traffic_127kx47.json
+    for path in (args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}.json")):
+        try:
+            with open(path) as fh:
+                tr = json.load(fh)
+        except (OSError, ValueError):
+            continue
         if tr.get("workload") == args.config and tr.get("tracers", 1) == args.tracers and \
-                dom in tr.get("bytes_per_launch", {}):
+                args.mesh == "structured" and not args.parity_levels and args.vlimit == 1 and \
+                args.fct_iter == 1 and dom in tr.get("bytes_per_launch", {}):
             traffic = tr["bytes_per_launch"][dom]
-    except (OSError, ValueError):
-        pass
+            break
     roof = None
     if dom in kb:
         avg_s = stats[dom][1] / stats[dom][0] * 1e-3
