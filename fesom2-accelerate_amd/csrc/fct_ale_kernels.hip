@@ -1388,6 +1388,15 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, a.nl - 1, a.vlimit, false);
     const bool NT = (env_int("FESOM2_NT", 6) & 1) != 0;
+    if constexpr (C == 2 && RB == 2 && EB == 2) {
+        // FESOM2_NL_PAIR: fct_adf_v / area_inv as 16-byte pairs at 8-byte alignment (ld_nl), as p1v
+        if (env_int("FESOM2_NL_PAIR", 1)) {
+            if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+            if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+            if (NT) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        }
+    }
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
     if (NT) F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, true>), groups, G, S, lds, s, mp, a, G, invS);
