@@ -50,6 +50,22 @@ def main():
               f"two streams {two:.4f} ms/pass ({100 * (two / one - 1):+.1f} %)", flush=True)
     ea.free()
     eb.free()
+    # batched tracers (BASELINE config 3): one batch of 2T on one stream vs two batches of T on two
+    T = int(os.environ.get("OVERLAP_BATCH", "3"))
+    if T > 0:
+        trs = synth.make_tracer_fields(m, 2 * T)
+        whole = engine.FctAleBatch(dm, trs, stream=sa)
+        ha = engine.FctAleBatch(dm, trs[:T], stream=sa)
+        hb = engine.FctAleBatch(dm, trs[T:], stream=sb)
+        run([whole], 2)
+        run([ha, hb], 2)
+        for rnd in range(3):
+            one = run([whole], K // 2) / (K // 2)
+            two = run([ha, hb], K // 2) / (K // 2)
+            print(f"round {rnd}: {2 * T} tracers batched, one stream {one:.4f} ms/pass | two batches of {T} on two "
+                  f"streams {two:.4f} ms/pass ({100 * (two / one - 1):+.1f} %)", flush=True)
+        for e in (whole, ha, hb):
+            e.free()
     dm.free()
 
 
