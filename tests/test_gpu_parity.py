@@ -398,10 +398,10 @@ def test_sizes_beyond_int32():
     dll().fesom2_free_(h8.ref)
 
 
-def run_split(m, f):
+def run_split(m, f, vlimit=1):
     """The direction-split pass (bench default): fct_ale_pre_comm_v_acc_ -> fct_ale_post_comm_h_acc_."""
     dm = engine.DeviceMesh(m)
-    e = engine.FctAle(dm, f)
+    e = engine.FctAle(dm, f, vlimit=vlimit)
     try:
         assert e.pre_comm_v() == 7, abi.last_error()
         assert e.post_comm_h() == 9, abi.last_error()
@@ -427,6 +427,47 @@ def test_level_counts(nl, full, mode):
         st, got = run_pass(m, f, fused=mode == "fused")
         assert st == 9
     check_pass(m, got, O.full_pass(m, f))
+
+
+def degenerate_mesh(kind):
+    """Shallow columns the synthetic generator never makes: "one_level" (nl = 2, a single level per
+    column), "one_wet" (nl = 11 but every element has 2 levels: one wet cell per column, the rest of
+    each column dry), "shallow_region" (a band of elements with 2 levels, so whole nodes have one wet
+    level next to deep ones)."""
+    import dataclasses
+    if kind == "one_level":
+        m = synth.make_mesh(16, 8, 3, full_depth=True)
+        return dataclasses.replace(m, nl=2, nlev_elem=np.full_like(m.nlev_elem, 2), nlev_nod=np.full_like(m.nlev_nod, 2),
+                                   name="16x8x1")
+    m = synth.make_mesh(40, 14, 11, full_depth=kind == "one_wet")
+    le = m.nlev_elem.copy()
+    if kind == "one_wet":
+        le[:] = 2
+    else:
+        le[: le.size // 3] = 2
+    en = m.elem2D_nodes.reshape(-1, 3) - 1
+    ln = np.zeros(m.N, np.int64)
+    np.maximum.at(ln, en.reshape(-1), np.repeat(le, 3).astype(np.int64))
+    return dataclasses.replace(m, nlev_elem=le.astype(np.int32), nlev_nod=ln.astype(np.int32), name=kind)
+
+
+@pytest.mark.parametrize("kind", ["one_level", "one_wet", "shallow_region"])
+@pytest.mark.parametrize("mode", ["split", "split_internal", "fused", "sequence", "stepwise", "vlimit2", "vlimit3"])
+def test_degenerate_level_counts(kind, mode, monkeypatch):
+    """Columns with one level or one wet cell: every path equals the oracle (b3v limits nz = 1 only,
+    the a3 stencil has no interior levels, b1v reads the bottom interface)."""
+    m = degenerate_mesh(kind)
+    if kind == "shallow_region":
+        assert (m.nlev_nod == 2).any() and (m.nlev_nod > 2).any()
+    f = synth.make_fields(m)
+    monkeypatch.setenv("FESOM2_P1V_B3H", "1" if mode == "split_internal" else "0")
+    vl = int(mode[-1]) if mode.startswith("vlimit") else 1
+    if mode.startswith("split") or mode.startswith("vlimit"):
+        got = run_split(m, f, vlimit=vl)
+    else:
+        st, got = run_pass(m, f, fused=mode == "fused", path="stepwise" if mode == "stepwise" else "fused")
+        assert st == 9, abi.last_error()
+    check_pass(m, got, O.full_pass(m, f, vlimit=vl))
 
 
 SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1V_EARLY": "8"},
