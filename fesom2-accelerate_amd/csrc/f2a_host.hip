@@ -325,13 +325,15 @@ bool capture_open(hipStream_t s)
 
 bool capture_close(hipStream_t s, CaptureLog *log)
 {
+    // only the thread that opened the capture closes it: its thread-local pointer to the capture's
+    // log must not outlive the log
     std::lock_guard<std::mutex> lock(g_cap_mutex);
     for (size_t k = 0; k < g_caps.size(); k++)
-        if (g_caps[k]->origin == s && s) {
+        if (g_caps[k]->origin == s && s && g_caps[k] == t_cap) {
             OpenCapture *c = g_caps[k];
             *log = std::move(c->log);
             g_caps.erase(g_caps.begin() + k);
-            if (t_cap == c) t_cap = nullptr;
+            t_cap = nullptr;
             delete c;
             return true;
         }
@@ -343,6 +345,7 @@ void timing_begin(const char *name, hipStream_t s, void **token)
     auto *t = new TimedLaunch;
     t->name = name;
     if (hipEventCreate(&t->start) != hipSuccess || hipEventCreate(&t->stop) != hipSuccess) {
+        if (t->start) (void)hipEventDestroy(t->start);
         delete t;
         *token = nullptr;
         return;

@@ -1057,7 +1057,7 @@ void fesom2_graph_end_(int *istat, void **s, void **graph)
     const hipStream_t st = stream_of(s);
     auto *g = new GraphHandle;
     if (!capture_close(st, &g->log)) {
-        report("fesom2_graph_end_: the stream has no capture opened by fesom2_graph_begin_");
+        report("fesom2_graph_end_: the stream has no capture opened by fesom2_graph_begin_ on this thread");
         delete g;
         return;
     }
