@@ -526,7 +526,8 @@ def main():
     dom = max(stats, key=lambda k: stats[k][1]) if stats else None
     traffic = None
     slug = args.config.replace(" ", "").replace(".", "p")  # "127k x 47" -> profiles/traffic_127kx47.json
-    for path in (args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}.json")):
+    for path in (args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}.json"),
+                 os.path.join(ROOT, "profiles", f"traffic_{slug}_{args.tracers}tr.json")):
         try:
             with open(path) as fh:
                 tr = json.load(fh)
