@@ -339,7 +339,16 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
     // per lane, exclusive scan of ceil(lev/C)) while the records load.
     int4 *ie_ent = reinterpret_cast<int4 *>(lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)));
     int *ie_off = reinterpret_cast<int *>(ie_ent + kMaxInternal);  // [kMaxInternal + 1]: + total
-    if constexpr (VERT && (OPT & 16)) {
+    // OPT & 32: the entries go global -> LDS by DMA after the records barrier instead (no VGPRs, off
+    // the records' critical path: the two dependent loads above delay the block's first barrier),
+    // and wave 0 scans their slot counts after the first barrier (read after the third)
+    int int_i0 = 0, int_n = 0;
+    if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
+        const int blk = first / G;
+        int_i0 = mp.int_ptr[blk];  // block-uniform: scalar loads, waited for at the records barrier
+        int_n = mp.int_ptr[blk + 1] - int_i0;
+    }
+    if constexpr (VERT && (OPT & 16) && !(OPT & 32)) {
         if (t < kWave) {
             const int blk = first / G, i0 = mp.int_ptr[blk], n = mp.int_ptr[blk + 1] - i0;
             const int4 ent = t < n ? mp.int_edges[i0 + t] : make_int4(0, 0, 0, 0);
@@ -362,6 +371,12 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
     real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
+    if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
+        if (t < int_n)  // wave 0 (int_n <= kMaxInternal = kWave): lane t's entry lands at ie_ent[t]
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(mp.int_edges + int_i0 + t),
+                (__attribute__((address_space(3))) void *)ie_ent, 16, 0, 0);
+    }
     int j, u;
     slot_of(t, S, invS, j, u);
     const int z0 = C * u;
@@ -480,6 +495,19 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             }
     }
     __syncthreads();
+    if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
+        if (t < kWave) {  // the DMA'd entries (landed: the barrier waited for vmcnt) -> slot offsets
+            const int sl = t < int_n ? (ie_ent[t].w + C - 1) / C : 0;
+            int incl = sl;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const int v = __shfl_up(incl, d);
+                if (t >= d) incl += v;
+            }
+            if (t < kMaxInternal) ie_off[t] = incl - sl;
+            if (t == kWave - 1) ie_off[kMaxInternal] = incl;
+        }
+    }
     if (!VERT && nw == 0) return;
     real op[C], om[C];
 #pragma unroll
@@ -1473,6 +1501,8 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
         const float inv = 1.0f / (float)S;
         if ((env_int("FESOM2_NT", 6) & 4) != 0) {  // non-temporal single-use streams (see below)
+            if (in && env_int("FESOM2_P1V_INT_DMA", 1))  // internal-edge entries staged by DMA (OPT & 32)
+                F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv);
             if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
         }
@@ -1505,6 +1535,8 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (C == 2) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     }
+    if (in && C == 2 && early == 4 && nt && env_int("FESOM2_P1V_INT_DMA", 1))
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2 && early == 4 && nt)
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2 && early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
