@@ -326,7 +326,7 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
                                               const real *__restrict__ ttf, int z0, int L,
                                               real (&vx)[C], real (&vn)[C], bool last1 = false)
 {
-    const int zl = (ODD && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
+    const int zl = (ODD && C == 2 && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
     for (int r = r0; r < r1; r += kBatch) {
         size_t idx[kBatch];
         int lev[kBatch];
@@ -373,7 +373,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
                                           const real *__restrict__ adf_h, int z0, int L, F &&f,
                                           bool last1 = false)
 {
-    const int zl = (ODD && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
+    const int zl = (ODD && C == 2 && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
         size_t idx[kBatch];
         int code[kBatch];

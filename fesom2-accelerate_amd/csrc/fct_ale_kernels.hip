@@ -439,7 +439,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
-        const size_t bl = b - ((ODD && last1) ? 1 : 0);  // odd L: the last slot's pair starts a level early
+        const size_t bl = b - ((ODD && C == 2 && last1) ? 1 : 0);  // odd L: the last slot's pair starts a level early
         ldo_pre<C, ODD>(a.LO + bl, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
         ldo_pre<C, ODD>(a.ttf + bl, tt, last1);
         if constexpr (OPT & 1) {
@@ -639,7 +639,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
                     hnn[c] = me[2 * gl_n + c];
                 }
             } else {
-                const size_t bl = b - ((ODD && last1) ? 1 : 0);
+                const size_t bl = b - ((ODD && C == 2 && last1) ? 1 : 0);
                 ldo_s_pre<C, NT, ODD>(a.del_v + bl, del_v, last1);
                 ldo_s_pre<C, NT, ODD>(a.hnode + bl, hn, last1);
                 ldo_s_pre<C, NT, ODD>(a.hnode_new + bl, hnn, last1);
