@@ -885,15 +885,24 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
     int q[H], z0[H];
     bool act[H];
     real f[H][C], p1[H][C], m1[H][C], p2[H][C], m2[H][C];
+    // a block whose edges all carry every level (full depth: the common case) finds a slot's edge by
+    // division; otherwise by binary search over the slot offsets
+    const int Sf = (L + 1) / 2;
+    const bool uniform = n > 0 && s_off[n] == n * Sf;
 #pragma unroll
     for (int h = 0; h < H; h++) {
         const int slot = t + h * (int)blockDim.x;
         act[h] = n > 0 && slot < s_off[n];
-        int lo = 0, hi = n - 1;  // last edge with s_off <= slot
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_off[mid] <= slot) lo = mid;
-            else hi = mid - 1;
+        int lo = 0;
+        if (uniform) {
+            lo = min(slot / Sf, n - 1);
+        } else {
+            int hi = n - 1;  // last edge with s_off <= slot
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= slot) lo = mid;
+                else hi = mid - 1;
+            }
         }
         q[h] = lo;
         z0[h] = act[h] ? C * (slot - s_off[lo]) : 0;
