@@ -579,12 +579,19 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             // of them (b1h of both endpoint columns) is behind the first barrier, no other block
             // touches them, and both endpoints' final plus/minus are in LDS
             const int total = ie_off[kMaxInternal];
+            const int Sf = (L + C - 1) / C;  // slots of an edge that carries every level
+            // (OPT & 32, entry count known) all edges full depth: the item's entry by division
+            const bool uniform = (OPT & 32) && total == int_n * Sf;
             for (int w = t; w < total; w += (int)blockDim.x) {
                 int lo_k = 0, hi_k = kMaxInternal - 1;  // last entry with ie_off <= w
-                while (lo_k < hi_k) {
-                    const int mid = (lo_k + hi_k + 1) >> 1;
-                    if (ie_off[mid] <= w) lo_k = mid;
-                    else hi_k = mid - 1;
+                if (uniform) {
+                    lo_k = w / Sf;
+                } else {
+                    while (lo_k < hi_k) {
+                        const int mid = (lo_k + hi_k + 1) >> 1;
+                        if (ie_off[mid] <= w) lo_k = mid;
+                        else hi_k = mid - 1;
+                    }
                 }
                 const int4 e = ie_ent[lo_k];
                 const int zi = C * (w - ie_off[lo_k]);
