@@ -446,12 +446,29 @@ static bool pack_edges(const std::vector<int4> &einfo, const std::vector<int> &b
 
 // MeshPlanDev::b3p_* over p_edge_info: descriptors [0, b3p_nint) for the interior edges, the rest
 // for the boundary ones
+// slot count shared by every edge of einfo[e0, e1) if the greedy packing gave each of descriptors
+// [d0, d1) the next P = min(kB3hPackEdges, cap / slots) of them (the last fewer), else 0
+static int regular_slots(const std::vector<int4> &einfo, int e0, int e1, const std::vector<int2> &desc, int d0, int d1,
+                         int cap)
+{
+    if (e1 <= e0) return 0;
+    const int sl = (einfo[e0].z + 1) / 2;
+    for (int k = e0; k < e1; k++)
+        if ((einfo[k].z + 1) / 2 != sl) return 0;
+    const int P = std::min(kB3hPackEdges, cap / sl);
+    for (int k = d0; k < d1; k++)
+        if (desc[k].x != e0 + (k - d0) * P || desc[k].y != std::min(P, e1 - desc[k].x)) return 0;
+    return sl;
+}
+
 static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &einfo, int n_int)
 {
     std::vector<int2> desc;
     std::vector<unsigned short> off;
     std::vector<int> ends;
     if (!pack_edges(einfo, {0, n_int, (int)einfo.size()}, d.b3p_cap, desc, off, ends)) return false;
+    d.b3p_slots_int = regular_slots(einfo, 0, n_int, desc, 0, ends[0], d.b3p_cap);
+    d.b3p_slots_bnd = regular_slots(einfo, n_int, (int)einfo.size(), desc, ends[0], (int)desc.size(), d.b3p_cap);
     d.b3p_desc = plan->mem.upload(desc);
     d.b3p_off = plan->mem.upload(off);
     d.b3p_nint = ends[0];
@@ -930,6 +947,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 d.b3x_off = plan->mem.upload(xoff);
                 d.b3x_ndesc = (int)xdesc.size();
                 d.b3x_cap = xcap;
+                // regular packing (every block P consecutive edges): the b3h blocks then compute their
+                // slice instead of loading a descriptor (checked against the descriptors themselves)
+                d.b3x_slots = regular_slots(ext, 0, (int)ext.size(), xdesc, 0, (int)xdesc.size(), xcap);
                 if (!d.int_ptr || !d.int_edges || (!ext.empty() && (!d.p_edge_ext || !d.b3x_desc || !d.b3x_off)))
                     return fail("device allocation for the internal edge lists failed");
             } else {  // nothing to gain, or a block with too many: every interior edge crosses

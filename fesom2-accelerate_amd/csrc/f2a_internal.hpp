@@ -108,6 +108,8 @@ struct MeshPlanDev {
     const int2 *b3x_desc = nullptr;
     const unsigned short *b3x_off = nullptr;
     int b3x_ndesc = 0, b3x_cap = 0;
+    int b3x_slots = 0;  // > 0: every crossing edge has this many level-pair slots (regular packing)
+    int b3p_slots_int = 0, b3p_slots_bnd = 0;  // the same for b3p's interior / boundary edge ranges
     // b3-horizontal of the block-internal edges inside p1v (both endpoints' plus/minus are in the
     // block's LDS after b2): for p1v block b (int_G positions of the processing order) the entries
     // int_edges[int_ptr[b] .. int_ptr[b+1]) = {edge, column of edges(1,e), column of edges(2,e), lev}

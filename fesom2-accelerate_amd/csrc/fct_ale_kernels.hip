@@ -867,10 +867,14 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 // ceil(lev/2) level-pair slots (not L/2: shallow edges leave no idle slots), at most kB3hPackSlots
 // slots, two per thread (both slots' loads in flight together, as k_b3h_u's two groups).  The
 // block's edge infos and slot offsets go to LDS; a thread finds its edge by binary search.
-template <bool NT, bool ODD, int H = 2>
+// REG (reg = {P, s, first edge, edge count}): every edge of the list has s slots, so the greedy
+// packing gave each block P = min(kB3hPackEdges, cap / s) consecutive edges (the last block fewer):
+// a block computes its slice instead of loading a descriptor first, and drops the slot offsets.
+template <bool NT, bool ODD, int H = 2, bool REG = false>
 __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, const unsigned short *__restrict__ off,
                                                 const int4 *__restrict__ einfo, int L, const real *__restrict__ plus,
-                                                const real *__restrict__ minus, real *__restrict__ adf_h, Tracers trs)
+                                                const real *__restrict__ minus, real *__restrict__ adf_h, Tracers trs,
+                                                int4 reg)
 {
     __shared__ int4 s_ei[kB3hPackEdges];
     __shared__ int s_off[kB3hPackEdges + 1];
@@ -879,30 +883,40 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
     plus += tr * trs.node;
     minus += tr * trs.node;
     adf_h += tr * trs.edge;
-    const int2 dsc = desc[g];
-    const int t = threadIdx.x, n = dsc.y;
-    for (int i = t; i < n; i += blockDim.x) {
-        const int4 ei = einfo[dsc.x + i];
-        s_ei[i] = ei;
-        s_off[i] = off[dsc.x + i];
-        if (i == n - 1) s_off[n] = off[dsc.x + i] + (ei.z + 1) / 2;
+    const int t = threadIdx.x;
+    int n, Sf;
+    if constexpr (REG) {
+        const int start = reg.z + g * reg.x;
+        n = min(reg.x, reg.z + reg.w - start);
+        Sf = reg.y;
+        for (int i = t; i < n; i += blockDim.x) s_ei[i] = einfo[start + i];
+    } else {
+        const int2 dsc = desc[g];
+        n = dsc.y;
+        for (int i = t; i < n; i += blockDim.x) {
+            const int4 ei = einfo[dsc.x + i];
+            s_ei[i] = ei;
+            s_off[i] = off[dsc.x + i];
+            if (i == n - 1) s_off[n] = off[dsc.x + i] + (ei.z + 1) / 2;
+        }
+        // a block whose edges all carry every level (full depth: the common case) finds a slot's
+        // edge by division; otherwise by binary search over the slot offsets
+        Sf = (L + 1) / 2;
     }
     __syncthreads();
     constexpr int C = 2;
     int q[H], z0[H];
     bool act[H];
     real f[H][C], p1[H][C], m1[H][C], p2[H][C], m2[H][C];
-    // a block whose edges all carry every level (full depth: the common case) finds a slot's edge by
-    // division; otherwise by binary search over the slot offsets
-    const int Sf = (L + 1) / 2;
-    const bool uniform = n > 0 && s_off[n] == n * Sf;
+    const int total = REG ? n * Sf : (n > 0 ? s_off[n] : 0);
+    const bool uniform = REG || (n > 0 && total == n * Sf);
 #pragma unroll
     for (int h = 0; h < H; h++) {
         const int slot = t + h * (int)blockDim.x;
-        act[h] = n > 0 && slot < s_off[n];
+        act[h] = n > 0 && slot < total;
         int lo = 0;
         if (uniform) {
-            lo = min(slot / Sf, n - 1);
+            lo = min(slot / Sf, max(n - 1, 0));
         } else {
             int hi = n - 1;  // last edge with s_off <= slot
             while (lo < hi) {
@@ -912,7 +926,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
             }
         }
         q[h] = lo;
-        z0[h] = act[h] ? C * (slot - s_off[lo]) : 0;
+        z0[h] = act[h] ? C * (slot - (uniform ? lo * Sf : s_off[lo])) : 0;
     }
 #pragma unroll
     for (int h = 0; h < H; h++) {
@@ -1711,7 +1725,7 @@ hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int 
 // packed b3h over descriptors [d0, d1) of a list (k_b3h_p), or false if packing is off for this L
 static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const int4 *einfo, int cap, int d0, int d1,
                               int nl, const real *plus, const real *minus, real *adf_h, const Tracers &tr,
-                              hipStream_t s, hipError_t *err)
+                              hipStream_t s, hipError_t *err, int4 reg = make_int4(0, 0, 0, 0))
 {
     const int L = nl - 1;
     if (!desc || !env_int("FESOM2_B3H_PACK", 1) || !(L % 2 == 0 || odd_pairs(L))) return false;
@@ -1725,16 +1739,28 @@ static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const
     int H = env_int("FESOM2_B3HP_H", 2);
     if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
     const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
+    const int4 none = make_int4(0, 0, 0, 0);
+    // regular list (reg.x > 0: every edge the same slot count): no descriptor loads (FESOM2_B3HP_REG)
+    if (reg.x > 0 && H == 2 && NT && env_int("FESOM2_B3HP_REG", 1)) {
+        if (L % 2)
+            hipLaunchKernelGGL((k_b3h_p<true, true, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
+                               adf_h, tr, reg);
+        else
+            hipLaunchKernelGGL((k_b3h_p<true, false, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
+                               adf_h, tr, reg);
+        *err = hipGetLastError();
+        return true;
+    }
     if (H == 1)
-        hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+        hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
     else if (H == 4)
-        hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+        hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
     else if (L % 2)
-        hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+        hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
     else if (NT)
-        hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+        hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
     else
-        hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr);
+        hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
     *err = hipGetLastError();
     return true;
 }
@@ -1743,13 +1769,15 @@ hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
     // packed by depth (FESOM2_B3H_PACK=1): the plan's descriptors for exactly these edge ranges
-    int d0 = -1, d1 = -1;
-    if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc;
-    else if (begin == 0 && count == mp.n_edge_interior) d0 = 0, d1 = mp.b3p_nint;
-    else if (begin == mp.n_edge_interior && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc;
+    int d0 = -1, d1 = -1, sl = 0;  // sl: regular slot count of the edge range, if any
+    const int ni = mp.n_edge_interior;
+    if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc, sl = ni == mp.n_edges ? mp.b3p_slots_int : 0;
+    else if (begin == 0 && count == ni) d0 = 0, d1 = mp.b3p_nint, sl = mp.b3p_slots_int;
+    else if (begin == ni && begin + count == mp.n_edges) d0 = mp.b3p_nint, d1 = mp.b3p_ndesc, sl = mp.b3p_slots_bnd;
+    const int4 reg = sl > 0 ? make_int4(std::min(kB3hPackEdges, mp.b3p_cap / sl), sl, begin, count) : make_int4(0, 0, 0, 0);
     hipError_t err;
     if (d0 >= 0 && launch_b3h_packed(mp.b3p_desc, mp.b3p_off, mp.p_edge_info, mp.b3p_cap, d0, d1, nl, plus, minus,
-                                     adf_h, tr, s, &err))
+                                     adf_h, tr, s, &err, reg))
         return err;
     return launch_b3h_edges(mp.p_edge_info + begin, count, nl, plus, minus, adf_h, tr, s);
 }
@@ -1760,8 +1788,11 @@ hipError_t launch_b3h_ext(const MeshPlanDev &mp, int nl, const real *plus, const
     if (mp.n_ext_interior == 0) return hipSuccess;
     if (!mp.p_edge_ext) return hipErrorInvalidValue;
     hipError_t err;
+    const int4 reg = mp.b3x_slots > 0 ? make_int4(std::min(kB3hPackEdges, mp.b3x_cap / mp.b3x_slots), mp.b3x_slots, 0,
+                                                  mp.n_ext_interior)
+                                      : make_int4(0, 0, 0, 0);
     if (launch_b3h_packed(mp.b3x_desc, mp.b3x_off, mp.p_edge_ext, mp.b3x_cap, 0, mp.b3x_ndesc, nl, plus, minus, adf_h,
-                          tr, s, &err))
+                          tr, s, &err, reg))
         return err;
     return launch_b3h_edges(mp.p_edge_ext, mp.n_ext_interior, nl, plus, minus, adf_h, tr, s);
 }

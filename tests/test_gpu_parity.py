@@ -485,7 +485,7 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_P1V_B3H": "1", "FESOM2_CPT": "1"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3H_PACK": "0"},
                {"FESOM2_NT": "2"}, {"FESOM2_NT": "2", "FESOM2_P1V_B3H": "1"}, {"FESOM2_NT": "6", "FESOM2_P1V_B3H": "0"},
                {"FESOM2_BLOB": "1"}, {"FESOM2_BLOB": "1", "FESOM2_PATCH_ORDER": "1"}, {"FESOM2_BLOB": "0"},
-               {"FESOM2_P1V_B3H": "1", "FESOM2_P1V_INT_DMA": "0"}]
+               {"FESOM2_P1V_B3H": "1", "FESOM2_P1V_INT_DMA": "0"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3HP_REG": "0"}]
 
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
