@@ -1,8 +1,8 @@
 #!/bin/bash
-# Final round-2 bench lines (r02f: after the DMA staging and division fast paths) (run on the GPU box from the repo root): every --check run compares every
-# owned cell with the oracle.  Output: gpurun_out/r02f_<name>.json (+ .err)
+# Final round-2 bench lines (r02g: + regular b3h packing) (run on the GPU box from the repo root): every --check run compares every
+# owned cell with the oracle.  Output: gpurun_out/r02g_<name>.json (+ .err)
 set -e
-run() { name=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r02f_$name.json 2> gpurun_out/r02f_$name.err; tail -1 gpurun_out/r02f_$name.json | cut -c1-150; }
+run() { name=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r02g_$name.json 2> gpurun_out/r02g_$name.err; tail -1 gpurun_out/r02g_$name.json | cut -c1-150; }
 run default
 run 127k47_check --config "127k x 47" --check --no-cpu-baseline
 run 6tracers_check --tracers 6 --check --no-cpu-baseline
