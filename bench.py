@@ -198,62 +198,109 @@ def build_local(args, rank, world):
     return partition.local_mesh(g, part, rank)  # (local mesh, halo lists)
 
 
-def verify(args, e, step, m, fields, rank, world, dist):
-    """One pass on the pristine inputs, owned results gathered on rank 0 and compared cell for cell
-    with the oracle's single-domain pass over the global mesh (every tracer)."""
+def host_halo_exchange(dist, lists, cols):
+    """FESOM's exchange_nod over gloo for (NT, L) host arrays ``cols`` (owned columns to each
+    neighbour, its columns into our halo), in place.  Used by bench's --exchange host step and by the
+    per-rank oracle of the parity check (the same exchange test_partition.py checks against the
+    single-domain pass)."""
+    import torch
+    ops, bufs = [], {}
+    for q in lists.neighbors:
+        out = np.ascontiguousarray(np.stack([a[lists.send[q] - 1] for a in cols]))
+        bufs[q] = np.empty((len(cols), lists.recv[q].size) + cols[0].shape[1:])
+        ops.append(dist.P2POp(dist.isend, torch.from_numpy(out), q))
+        ops.append(dist.P2POp(dist.irecv, torch.from_numpy(bufs[q]), q))
+    for w in dist.batch_isend_irecv(ops) if ops else []:
+        w.wait()
+    for q in lists.neighbors:
+        for i, a in enumerate(cols):
+            a[lists.recv[q] - 1] = bufs[q][i]
+
+
+def oracle_local(m, fields, args, dist=None, lists=None):
+    """The oracle's pass for every tracer on this rank's local mesh (owned + one-ring halo), with the
+    plus/minus halo exchanged over gloo between phase 1 and phase 2 when N > 1 -- FESOM's own
+    sequence (docs/refactoring.md:199-200).  Local edges keep the global order, so this equals the
+    single-domain pass on every owned cell (tests/test_partition.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    out = []
+    for fk in fields:
+        if args.fct_iter > 1:  # 1 GPU (main() refuses it otherwise)
+            out.append(O.iterated_pass(m, fk, args.fct_iter))
+            continue
+        st, p1 = O.pre_comm(m, fk, vlimit=args.vlimit)
+        if st != 5:
+            raise RuntimeError(f"oracle pre_comm stopped at alg_state {st}")
+        if dist is not None and lists is not None:
+            host_halo_exchange(dist, lists, [p1["plus"].reshape(-1, m.L), p1["minus"].reshape(-1, m.L)])
+        r = O.post_comm(m, fk, p1["plus"], p1["minus"])
+        r.update(plus=p1["plus"], minus=p1["minus"])
+        out.append(r)
+    return out
+
+
+def compare_local(m, got, want):
+    """Cell-for-cell comparison of one rank's results with its oracle: plus/minus on the owned wet
+    cells, del_v/del_h/fct_adf_v on every owned cell, fct_adf_h on every local edge.  Returns
+    (mismatch counts per field, max |got - want|, cells compared)."""
+    L, nl = m.L, m.nl
+    wet = np.arange(L)[None, :] < (m.nlev_nod[: m.N, None].astype(np.int64) - 1)
+    bad, max_abs, cells = {}, 0.0, 0
+    for k, w in enumerate(want):
+        for name, width, rows, mask in (("plus", L, m.N, wet), ("minus", L, m.N, wet), ("del_v", L, m.N, None),
+                                        ("del_h", L, m.N, None), ("adf_v", nl, m.N, None),
+                                        ("adf_h", L, m.E, None)):
+            a = got[name][k][: rows * width].reshape(rows, width)
+            b = w[name][: rows * width].reshape(rows, width)
+            if mask is not None:
+                a, b = a[mask], b[mask]
+            diff = a != b
+            n = int(np.count_nonzero(diff))
+            cells += a.size
+            if n:
+                bad[name] = bad.get(name, 0) + n
+                with np.errstate(invalid="ignore"):
+                    d = np.abs(a[diff] - b[diff])
+                max_abs = max(max_abs, float(np.nanmax(d)) if np.isfinite(d).any() else float("inf"))
+    return bad, max_abs, cells
+
+
+def verify(args, e, step, m, fields, world, dist, lists, want=None):
+    """The reference harness's verify-before-report (kernels/fct_ale_b2.py:97-100, ``answer=``):
+    one pass on the pristine inputs, then every rank compares its owned cells (and local edges) with
+    the oracle run on its own local mesh -- in parallel on all ranks, the plus/minus halo exchanged
+    over gloo for the oracle -- and the counts are summed over ranks.  ``want``: the oracle's outputs
+    already computed for cpu_baseline (1 tracer, N = 1)."""
     for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h", "adf_v2", "adf_h2"):
         if name in e.host:
             e.upload(name)  # the host arrays were never touched in resident mode (adf_*2: zeros)
     step()
     abi.device_sync()
-    L, ntr = m.L, len(fields)
-
-    def per_tracer(name, width, rows):
-        a = e.download(name).reshape(ntr, -1, width)
-        return a[:, :rows] if rows is not None else a
-
-    mine = {"gid": m.node_gid[: m.N], "egid": m.edge_gid,
-            "plus": per_tracer("plus", L, m.N), "minus": per_tracer("minus", L, m.N),
-            "del_v": per_tracer("del_v", L, m.N), "del_h": per_tracer("del_h", L, m.N),
-            "adf_v": per_tracer("adf_v", m.nl, m.N), "adf_h": per_tracer("adf_h", L, None)}
+    ntr = len(fields)
+    got = {}
+    for name, width in (("plus", m.L), ("minus", m.L), ("del_v", m.L), ("del_h", m.L), ("adf_v", m.nl),
+                        ("adf_h", m.L)):
+        got[name] = e.download(name).reshape(ntr, -1)
+    t0 = time.perf_counter()
+    if want is None:
+        want = oracle_local(m, fields, args, dist if world > 1 else None, lists)
+    bad, max_abs, cells = compare_local(m, got, want)
+    t_oracle = time.perf_counter() - t0
     if dist is not None:
-        parts = [None] * world
-        dist.all_gather_object(parts, mine)
-    else:
-        parts = [mine]
-    if rank != 0:
-        return None
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    nx, ny, nl = global_dims(args, world)
-    g = delaunay(args, nx * ny, nl) if args.mesh != "structured" else \
-        synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels)
-    if args.permuted:  # the oracle runs on the same numbering (sums follow the local edge order)
-        g = synth.permute_mesh(g)
-    npos = np.empty(g.N, np.int64)
-    npos[g.node_gid] = np.arange(g.N)
-    epos = np.empty(g.E, np.int64)
-    epos[g.edge_gid] = np.arange(g.E)
-    wet = np.arange(L)[None, :] < (g.nlev_nod[:, None] - 1)
-    bad = {}
-    for k, fk in enumerate(synth.make_tracer_fields(g, ntr)):
-        want = O.iterated_pass(g, fk, args.fct_iter) if args.fct_iter > 1 else O.full_pass(g, fk, vlimit=args.vlimit)
-        for p in parts:
-            gid = npos[p["gid"]]
-            for name in ("plus", "minus"):
-                w = want[name].reshape(-1, L)[gid]
-                n = int(np.sum((p[name][k] != w) & wet[gid]))
-                if n:
-                    bad[name] = bad.get(name, 0) + n
-            for name, stride in (("del_v", L), ("del_h", L), ("adf_v", nl)):
-                n = int(np.sum(p[name][k] != want[name].reshape(-1, stride)[gid]))
-                if n:
-                    bad[name] = bad.get(name, 0) + n
-            n = int(np.sum(p["adf_h"][k] != want["adf_h"].reshape(-1, L)[epos[p["egid"]]]))
-            if n:
-                bad["adf_h"] = bad.get("adf_h", 0) + n
-    return {"exact": not bad, "mismatched_cells": bad, "tracers": ntr,
-            "against": "oracle full pass on the global mesh, per tracer"}
+        import torch
+        names = ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")
+        v = torch.tensor([bad.get(k, 0) for k in names] + [cells], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        mx = torch.tensor([max_abs], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        bad = {k: int(n) for k, n in zip(names, v.tolist()[:-1]) if n}
+        cells, max_abs = int(v[-1].item()), float(mx.item())
+    return {"exact": not bad, "max_abs": max_abs, "mismatched_cells": bad, "cells_compared": cells,
+            "tracers": ntr, "ranks": world, "oracle_s": round(t_oracle, 1),
+            "against": ("oracle/fct_ale_oracle.c pass on each rank's local mesh, plus/minus halo exchanged "
+                        "over gloo (per tracer)" if world > 1 else
+                        "oracle/fct_ale_oracle.c full pass on the same mesh (per tracer)")}
 
 
 def main():
@@ -293,9 +340,11 @@ def main():
                     help="FESOM2's iterative FCT (iter_yn, SURVEY.md 8(f) 1): a step is K-1 rounds of "
                          "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final pass (--path "
                          "split: the direction-split entries, fused: pre_comm -> post_comm_c); 1 GPU")
-    ap.add_argument("--check", action="store_true",
-                    help="after timing, rerun one pass on pristine inputs and compare every owned cell with the "
-                         "oracle on the global mesh (gathered over ranks)")
+    ap.add_argument("--check", action="store_true", default=True,
+                    help="(default) after timing, rerun one pass on pristine inputs and compare every owned cell and "
+                         "local edge with the oracle on each rank's local mesh; the line carries \"check\" and the "
+                         "exit status is 1 on any mismatch")
+    ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity check")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
                     help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "
                          "over gloo (validation only: lets N ranks share one GPU, which RCCL refuses)")
@@ -384,24 +433,18 @@ def main():
         dist.broadcast(t, src=0)
         C.memmove(uid, bytes(t.numpy().tobytes()), 128)
         halo = engine.Halo(uid, rank, world, lists, m.nl)
+        ci = halo.info()
         log(f"rank {rank}: owned {m.N} halo {m.H} neighbours {lists.neighbors} "
-            f"send {[lists.send[q].size for q in lists.neighbors]} recv {[lists.recv[q].size for q in lists.neighbors]}")
+            f"send {[lists.send[q].size for q in lists.neighbors]} recv {[lists.recv[q].size for q in lists.neighbors]} "
+            f"rccl {ci}")
+        if ci["nranks"] != world or ci["rank"] != rank:
+            raise SystemExit(f"RCCL communicator reports rank {ci['rank']} of {ci['nranks']}, expected {rank} of {world}")
 
     def host_exchange():
         """fct_plus/fct_minus halo through host memory and gloo (--exchange host)."""
         abi.device_sync()
         pm = [e.download(k).reshape(args.tracers, -1, m.L) for k in ("plus", "minus")]
-        ops, bufs = [], {}
-        for q in lists.neighbors:
-            out = np.ascontiguousarray(np.stack([a[:, lists.send[q] - 1] for a in pm]))
-            bufs[q] = np.empty((2, args.tracers, lists.recv[q].size, m.L))
-            ops.append(dist.P2POp(dist.isend, torch.from_numpy(out), q))
-            ops.append(dist.P2POp(dist.irecv, torch.from_numpy(bufs[q]), q))
-        for w in dist.batch_isend_irecv(ops) if ops else []:
-            w.wait()
-        for q in lists.neighbors:
-            for i, a in enumerate(pm):
-                a[:, lists.recv[q] - 1] = bufs[q][i]
+        host_halo_exchange(dist, lists, [a[k] for a in pm for k in range(args.tracers)])
         e.upload("plus", pm[0].reshape(-1))
         e.upload("minus", pm[1].reshape(-1))
 
@@ -554,10 +597,13 @@ def main():
 
     # ---- CPU baseline (rank 0, N = 1 only)
     cpu = None
+    oracle_want = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
-        best, reps = O.time_full_pass(m, f, budget_s=args.cpu_budget)
+        best, reps, last = O.time_full_pass(m, f, budget_s=args.cpu_budget, keep=True)
+        if args.tracers == 1 and args.vlimit == 1 and args.fct_iter == 1 and not args.transfers:
+            oracle_want = [last]  # the parity check compares the GPU pass with this very pass
         cpu = {"value": round(s["cn"] / best, 1), "unit": "cell-updates/s", "cores": 1, "kind": "port",
                "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
                          f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)",
@@ -571,8 +617,9 @@ def main():
                           f"best of 2 ({t_ref:.2f} s per phase 1)"}
 
     check = None
-    if args.check:
-        check = verify(args, e, step, m, fields, rank, world, dist)  # a replay when --graph
+    if args.check and not args.transfers:  # --transfers: outputs land in the input host arrays
+        check = verify(args, e, step, m, fields, world, dist, lists, oracle_want)  # a replay when --graph
+        log(f"check: {check}")
     if graph is not None:
         graph.free()
 
@@ -611,6 +658,10 @@ def main():
         }
         if check is not None:
             out["check"] = check
+        if halo is not None:
+            ci = halo.info()
+            out["rccl_nranks"] = ci["nranks"]  # ncclCommCount of the communicator the exchange ran on
+            out["rccl"] = ci
         print(json.dumps(out), flush=True)
 
     e.free()
@@ -621,6 +672,8 @@ def main():
         halo.free()
     if dist is not None:
         dist.destroy_process_group()
+    if check is not None and not check["exact"]:
+        sys.exit(1)  # a fast wrong answer is not a result
 
 
 if __name__ == "__main__":

@@ -20,8 +20,8 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 
 // Bijective XCD-aware swizzle: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // residue class a contiguous range of tiles.  Speed only, never correctness.
-static __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements)
-// FESOM2_ABLATE (timing-only builds of an experiment, results are wrong): bit 0 skips the cluster
+static __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements, tuning build)
+// FESOM2_ABLATE (tuning build, timing-only experiments, results are wrong): bit 0 skips the cluster
 // gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2, bit 3 the arrival
 // counters of the fused b3h.
 static __constant__ int c_ablate = 0;
@@ -35,26 +35,22 @@ __device__ __forceinline__ int xcd_tile(int b, int G)
     return x * q + (x < r ? x : r) + k;
 }
 
+// the tuning build's knobs of the __constant__ switches above (the product keeps the defaults)
 static void init_swizzle()
 {
+#if F2A_TUNING
     static bool done = false;
     if (done) return;
     done = true;
-    const char *e = getenv("FESOM2_XCD");
-    if (e && atoi(e) == 0) {
+    if (knob("FESOM2_XCD", 1) == 0) {
         const int zero = 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_xcd_swizzle), &zero, sizeof zero);
     }
-    const char *tm = getenv("FESOM2_TRACER_MAJOR");
-    if (tm) {
-        const int v = atoi(tm);
+    if (const int v = knob("FESOM2_TRACER_MAJOR", -1); v >= 0)
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_major), &v, sizeof v);
-    }
-    const char *ab = getenv("FESOM2_ABLATE");
-    if (ab && atoi(ab)) {
-        const int v = atoi(ab);
+    if (const int v = knob("FESOM2_ABLATE", 0); v != 0)
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ablate), &v, sizeof v);
-    }
+#endif
 }
 
 __device__ __forceinline__ int wave_item()
@@ -594,17 +590,14 @@ __device__ __forceinline__ void p2_node_work(const MeshPlanDev &mp, P2Args &a, c
 // ---- host-side launch utilities
 static inline unsigned threads_for(int G, int S) { return (unsigned)(((G * S + kWave - 1) / kWave) * kWave); }
 
+// odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0 in the tuning
+// build: one level per thread)
+static inline bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && knob("FESOM2_ODD_PAIR", 1) != 0; }
+
 static inline int levels_per_thread(int L)
 {
-    const char *e = getenv("FESOM2_CPT");
-    if (e && atoi(e) == 1) return 1;
+    if (knob("FESOM2_CPT", 0) == 1) return 1;  // one level per thread (tuning build only)
     return (L % 2 == 0) ? 2 : 1;
-}
-
-static int env_int(const char *name, int dflt)
-{
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
 }
 
 #define F2A_LAUNCH_GROUPS(kernel, groups, G, L, lds_bytes, s, ...)                                       \

@@ -59,11 +59,6 @@ int kernel_path()
 
 void set_kernel_path(int p) { g_path = p == 1 ? 1 : 0; }
 
-int num_kernels_limit()
-{
-    const char *p = getenv("FESOM2_NUM_KERNELS");  // reference NUM_KERNELS, src/fesom2-accelerate.cu:256
-    return p ? atoi(p) : 10;
-}
 
 Buffer *buf(void **h, const char *name)
 {
@@ -259,10 +254,33 @@ struct OpenCapture {
     hipStream_t origin = nullptr;
     unsigned long long id = 0;  // hipStreamGetCaptureInfo id, shared by streams forked into it
     CaptureLog log;
+    bool orphaned = false;      // ended by another thread: the opening thread frees it
 };
 std::mutex g_cap_mutex;
 std::vector<OpenCapture *> g_caps;
 thread_local OpenCapture *t_cap = nullptr;  // the capture this thread opened
+
+// this thread's open capture (g_cap_mutex held); forgets one another thread has ended
+OpenCapture *my_capture()
+{
+    if (t_cap && t_cap->orphaned) {
+        delete t_cap;
+        t_cap = nullptr;
+    }
+    return t_cap;
+}
+
+// the open capture stream s belongs to (g_cap_mutex held), or nullptr
+OpenCapture *capture_of(hipStream_t s)
+{
+    if (!s) return nullptr;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(s, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return nullptr;
+    for (OpenCapture *c : g_caps)
+        if (c->id == id) return c;
+    return nullptr;
+}
 
 void add_unique(std::vector<CapturedUse> &v, const void *p, uint64_t serial)
 {
@@ -289,27 +307,93 @@ void note_use(const void *p, uint64_t serial)
 {
     if (!t_cap) return;
     std::lock_guard<std::mutex> lock(g_cap_mutex);
-    add_unique(t_cap->log.uses, p, serial);
+    if (OpenCapture *c = my_capture()) add_unique(c->log.uses, p, serial);
 }
 
 bool defer_event_wait(Buffer *b, hipStream_t s)
 {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    unsigned long long id = 0;
-    if (hipStreamGetCaptureInfo(s, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return false;
     std::lock_guard<std::mutex> lock(g_cap_mutex);
-    for (OpenCapture *c : g_caps)
-        if (c->id == id) {
-            add_unique(c->log.waits, b, b->serial);
-            add_unique(c->log.uses, b, b->serial);
-            return true;
+    OpenCapture *c = capture_of(s);
+    if (!c) return false;
+    add_unique(c->log.waits, b, b->serial);
+    add_unique(c->log.uses, b, b->serial);
+    return true;
+}
+
+// the capture log's record of b's mark (g_cap_mutex held), created at the first access
+static CapturedMark &mark_record(OpenCapture *c, Buffer *b, bool read)
+{
+    for (CapturedMark &m : c->log.marks)
+        if (m.b == b) return m;
+    CapturedMark m{b, b->serial, b->int_plan, b->int_serial};
+    m.read_first = read;
+    c->log.marks.push_back(m);
+    return c->log.marks.back();
+}
+
+void mark_internal(Buffer *adf_h, const Plan *plan, hipStream_t s)
+{
+    if (s) {
+        std::lock_guard<std::mutex> lock(g_cap_mutex);
+        if (OpenCapture *c = capture_of(s)) {
+            CapturedMark &m = mark_record(c, adf_h, false);
+            m.written = true;
+            m.final_mark = plan;
+            m.final_serial = plan ? plan->serial : 0;
         }
-    return false;
+    }
+    adf_h->int_plan = plan;
+    adf_h->int_serial = plan ? plan->serial : 0;
+}
+
+static void note_mark_read(Buffer *adf_h, hipStream_t s)
+{
+    if (!s) return;
+    std::lock_guard<std::mutex> lock(g_cap_mutex);
+    if (OpenCapture *c = capture_of(s)) (void)mark_record(c, adf_h, true);
+}
+
+bool has_internal(Buffer *adf_h, hipStream_t s)
+{
+    note_mark_read(adf_h, s);
+    return adf_h->int_plan != nullptr;
+}
+
+const Plan *peek_internal(Buffer *adf_h, hipStream_t s)
+{
+    note_mark_read(adf_h, s);
+    const void *p = adf_h->int_plan;
+    return p && object_live(p, adf_h->int_serial) ? static_cast<const Plan *>(p) : nullptr;
+}
+
+bool marks_replayable(const CaptureLog &log)
+{
+    for (const CapturedMark &m : log.marks)
+        if (m.read_first && object_live(m.b, m.serial) &&
+            (m.b->int_plan != m.entry || m.b->int_serial != m.entry_serial)) {
+            report("fesom2_graph_launch_: the graph's first use of fct_adf_h expects it %s by "
+                   "fct_ale_pre_comm_v_acc_, but it is %s now (run the matching phase first, or capture both)",
+                   m.entry ? "marked" : "not marked", m.b->int_plan ? "marked" : "not marked");
+            return false;
+        }
+    return true;
+}
+
+void marks_apply(const CaptureLog &log)
+{
+    for (const CapturedMark &m : log.marks)
+        if (m.written && object_live(m.b, m.serial)) {
+            m.b->int_plan = m.final_mark;
+            m.b->int_serial = m.final_serial;
+        }
 }
 
 bool capture_open(hipStream_t s)
 {
-    if (t_cap) return false;
+    {
+        std::lock_guard<std::mutex> lock(g_cap_mutex);
+        if (my_capture()) return false;
+    }
     auto *c = new OpenCapture;
     c->origin = s;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -323,20 +407,32 @@ bool capture_open(hipStream_t s)
     return true;
 }
 
-bool capture_close(hipStream_t s, CaptureLog *log)
+bool capture_close(hipStream_t s, CaptureLog *log, bool *foreign)
 {
-    // only the thread that opened the capture closes it: its thread-local pointer to the capture's
-    // log must not outlive the log
+    // the opening thread's thread-local pointer must not outlive the capture: a capture another
+    // thread opened is only unregistered here and marked orphaned; that thread frees it
+    *foreign = false;
     std::lock_guard<std::mutex> lock(g_cap_mutex);
-    for (size_t k = 0; k < g_caps.size(); k++)
-        if (g_caps[k]->origin == s && s && g_caps[k] == t_cap) {
-            OpenCapture *c = g_caps[k];
-            *log = std::move(c->log);
-            g_caps.erase(g_caps.begin() + k);
-            t_cap = nullptr;
-            delete c;
-            return true;
+    for (size_t k = 0; k < g_caps.size(); k++) {
+        OpenCapture *c = g_caps[k];
+        if (!s || c->origin != s) continue;
+        // capturing changed no mark: put back what the captured calls wrote
+        for (const CapturedMark &m : c->log.marks)
+            if (m.written && object_live(m.b, m.serial)) {
+                m.b->int_plan = m.entry;
+                m.b->int_serial = m.entry_serial;
+            }
+        g_caps.erase(g_caps.begin() + k);
+        if (c != t_cap) {
+            c->orphaned = true;
+            *foreign = true;
+            return false;
         }
+        *log = std::move(c->log);
+        t_cap = nullptr;
+        delete c;
+        return true;
+    }
     return false;
 }
 
@@ -416,13 +512,13 @@ static bool pack_edges(const std::vector<int4> &einfo, const std::vector<int> &b
     desc.clear();
     ends.clear();
     off.assign(einfo.size(), 0);
-    const char *cenv = getenv("FESOM2_B3HP_CAP");  // level pairs per block (A/B; default kB3hPackSlots)
+    const int cenv = knob("FESOM2_B3HP_CAP", kB3hPackSlots);  // level pairs per block (tuning build A/B)
     // at least one edge of the deepest kind per block (else no block could take it), and at most
     // 2048 pairs = a 1024-thread block at two slots per thread (the launch falls back to two slots
     // per thread whenever one slot per thread would need more than 1024 threads)
     int lmax = 0;
     for (const int4 &ei : einfo) lmax = std::max(lmax, ei.z);
-    cap = std::max({64, (lmax + 1) / 2, std::min(cenv ? atoi(cenv) : kB3hPackSlots, 2048)});
+    cap = std::max({64, (lmax + 1) / 2, std::min(cenv, 2048)});
     for (size_t part = 0; part + 1 < bounds.size(); part++) {
         int k = bounds[part];
         const int k_end = bounds[part + 1];
@@ -480,6 +576,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                                  int n_csr, int nl, std::string &err)
 {
     auto plan = std::make_unique<Plan>();
+    // plan option FESOM2_NUM_KERNELS: the stepwise path stops phase 1 after that many reference
+    // steps (the reference's NUM_KERNELS macro, src/fesom2-accelerate.cu:256; alg_state bisection)
+    if (const char *nk = getenv("FESOM2_NUM_KERNELS")) plan->num_kernels = atoi(nk);
     MeshPlanDev &d = plan->dev;
     d.n_owned = n_owned;
     d.n_total = n_total;
@@ -582,7 +681,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             rptr[n + 1] = (int)ring.size();
         }
         // does every owned node's cluster equal {n} + its edge neighbours, on the edges' levels?
-        if (n_csr >= n_owned) {
+        // (the tuning build's edge-list phase 1, FESOM2_P1_EDGE)
+        if (F2A_TUNING && n_csr >= n_owned) {
             bool same = true;
             for (int n = 0; n < n_owned && same; n++) {
                 const int ne = ptr[n + 1] - ptr[n], nr = rptr[n + 1] - rptr[n];
@@ -640,22 +740,23 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 local_numbering = gap[gap.size() / 2] <= std::max(n_owned / 64, 64);
             }
         }
+        // plan option FESOM2_PATCH (nodes per patch; 1 = index order), read when the plan is built
         const char *env = getenv("FESOM2_PATCH");
         const int patch = env ? atoi(env) : (local_numbering ? 16384 : 4096);
-        const char *senv = getenv("FESOM2_SUBPATCH");
-        const int sub = senv ? atoi(senv) : 0;
-        // FESOM2_BLOB=1: cut each patch into compact blobs of one p1v block (greedy: the next node
-        // is the unassigned patch neighbour with the most edges into the blob), so more edges have
-        // both endpoints in one p1v block (limited there, see MeshPlanDev::int_ptr)
-        const char *benv = getenv("FESOM2_BLOB");
-        const int blob_g = (benv && atoi(benv) != 0) ? p1v_group_columns(nl) : 0;
+        // tuning build: FESOM2_SUBPATCH (compact BFS blobs of that many nodes inside a patch) and
+        // FESOM2_BLOB=1 (compact blobs of one p1v block: the next node is the unassigned patch
+        // neighbour with the most edges into the blob, so more edges have both endpoints in one p1v
+        // block and are limited there, see MeshPlanDev::int_ptr) -- both measured neutral
+        const int sub = knob("FESOM2_SUBPATCH", 0);
+        const int blob_g = knob("FESOM2_BLOB", 0) != 0 ? p1v_group_columns(nl) : 0;
         std::vector<int> in_patch, bscore;
         if (blob_g > 1) {
             in_patch.assign(n_owned, -1);
             bscore.assign(n_owned, 0);
         }
-        const char *oenv = getenv("FESOM2_PATCH_ORDER");
-        const int porder = oenv ? atoi(oenv) : (local_numbering ? 0 : 1);
+        // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
+        // tuning build
+        const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);
         std::vector<int> order;
         std::vector<int> stamp, bq;  // FESOM2_PATCH_ORDER = 1: patch membership stamps, BFS queue
         if (porder == 1) stamp.assign(n_owned, -1);
@@ -825,7 +926,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         }
         for (int e = 0; e < n_edges; e++)
             if (!etaken[e]) push_edge(e);
-        // edges in owner order (chunked phase 2: an edge belongs to its first visited endpoint)
+#if F2A_TUNING
+        // edges in owner order (the tuning build's chunked phase 2, node-centric b3h and fused p2h:
+        // an edge belongs to its first visited endpoint)
         d.p_edge_owner = plan->mem.upload(einfo);
         d.p_owner_cum = plan->mem.upload(plan->owner_cum);
         if (!d.p_edge_owner || !d.p_owner_cum) return fail("device allocation for the edge order failed");
@@ -887,10 +990,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             d.wf_deps = plan->mem.upload(deps);
             if (!d.wf_edges || !d.wf_cross || !d.wf_edge_ptr || !d.wf_dep_ptr || !d.wf_deps)
                 return fail("device allocation for the persistent phase-2 plan failed");
-            if (getenv("FESOM2_PLAN_STATS"))
+            if (knob("FESOM2_PLAN_STATS", 0))
                 fprintf(stderr, "fesom2-accelerate: wavefront G=%d tiles=%d cross edges=%zu deps/tile %.2f\n", WG, ntiles,
                         cross.size(), (double)deps.size() / std::max(ntiles, 1));
         }
+#endif
         // interior / boundary split for the exchange overlap (stable: processing order kept), the
         // interior part split again into edges crossing p1v blocks and edges inside one p1v block
         // (both endpoints among the same int_G positions: p1v limits those itself, see int_ptr)
@@ -955,7 +1059,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             } else {  // nothing to gain, or a block with too many: every interior edge crosses
                 d.n_ext_interior = d.n_edge_interior;
             }
-            if (getenv("FESOM2_PLAN_STATS"))
+            if (knob("FESOM2_PLAN_STATS", 0))
                 fprintf(stderr, "fesom2-accelerate: p1v G=%d internal edges %d of %d interior (max %d per block)\n", IG,
                         d.n_edge_interior - d.n_ext_interior, d.n_edge_interior, most);
         } else {
@@ -970,8 +1074,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             for (int q = 0; q < kRecEdge && info[k].e0 + q < info[k].e1; q++) r.edge[q] = pedges[info[k].e0 + q];
         }
         d.node_rec = plan->mem.upload(recs);
-        // cluster staging plan for phase 1 (see MeshPlanDev::stage_*)
-        if (with_ring) {
+        // cluster staging plan for phase 1 (see MeshPlanDev::stage_*; the tuning build's
+        // FESOM2_P1_STAGE)
+        if (F2A_TUNING && with_ring) {
             const int SG = f2a::fused_group_columns(nl);
             std::vector<int> bptr(1, 0), bnodes;
             std::vector<NodeRec> srecs(recs);
@@ -993,7 +1098,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 umax = std::max(umax, (int)bnodes.size() - base);
                 bptr.push_back((int)bnodes.size());
             }
-            if (getenv("FESOM2_PLAN_STATS"))
+            if (knob("FESOM2_PLAN_STATS", 0))
                 fprintf(stderr, "fesom2-accelerate: staging G=%d blocks=%zu union mean %.2f max %d, ring mean %.2f\n", SG,
                         bptr.size() - 1, (double)bnodes.size() / std::max<size_t>(bptr.size() - 1, 1), umax,
                         (double)pring.size() / std::max(n_owned, 1));
@@ -1115,17 +1220,6 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
     return p;
 }
 
-void mark_internal(Buffer *adf_h, const Plan *plan)
-{
-    adf_h->int_plan = plan;
-    adf_h->int_serial = plan ? plan->serial : 0;
-}
-
-const Plan *peek_internal(const Buffer *adf_h)
-{
-    const void *p = adf_h->int_plan;
-    return p && object_live(p, adf_h->int_serial) ? static_cast<const Plan *>(p) : nullptr;
-}
 
 
 void drop_plans_of(const Buffer *b)

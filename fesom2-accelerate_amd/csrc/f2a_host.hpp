@@ -29,9 +29,8 @@ unsigned long error_count();  // number of report() calls so far (all threads)
 
 // ---- global modes
 extern int g_resident;  // fesom2_set_resident_
-int kernel_path();      // 0 fused, 1 stepwise
+int kernel_path();      // 0 fused, 1 stepwise (fesom2_set_path_; FESOM2_PATH, read once, sets the default)
 void set_kernel_path(int p);
-int num_kernels_limit();
 
 // ---- handles
 Buffer *buf(void **h, const char *name);
@@ -73,15 +72,37 @@ struct CapturedUse {
     const void *p;
     uint64_t serial;
 };
+// fct_adf_h's internal-edge mark (Buffer::int_plan) as a capture saw it.  The mark is host state,
+// so a replay has to reproduce it: the captured calls' last write is applied after every launch,
+// and when the capture's first access was a read (a captured post_comm_h after an eager
+// pre_comm_v), every launch first checks that the mark holds what the capture read.  At capture end
+// the mark is put back to its value before the capture: capturing is not running.
+struct CapturedMark {
+    Buffer *b;
+    uint64_t serial;                 // b's live-object serial
+    const void *entry;               // the mark before the capture touched it
+    uint64_t entry_serial;
+    bool read_first = false;         // the capture's first access read the mark
+    bool written = false;            // the capture wrote it; final = the last value written
+    const void *final_mark = nullptr;
+    uint64_t final_serial = 0;
+};
 struct CaptureLog {
     std::vector<CapturedUse> uses, waits;
+    std::vector<CapturedMark> marks;
 };
 // register an open capture whose origin is s (after hipStreamBeginCapture); false if this thread
 // already has one open
 bool capture_open(hipStream_t s);
 // unregister the capture whose origin is s and hand over its log; false if s is not the origin of
-// a capture opened by capture_open
-bool capture_close(hipStream_t s, CaptureLog *log);
+// a capture opened by capture_open on this thread.  A capture whose origin is s but which another
+// thread opened is unregistered as well (*foreign = true, return false): the caller ends the HIP
+// capture and drops the graph, and that thread's next library call forgets it.
+bool capture_close(hipStream_t s, CaptureLog *log, bool *foreign);
+// before every replay: the marks whose first captured access was a read must hold what the capture
+// read (false + report otherwise); after it: the captured final marks
+bool marks_replayable(const CaptureLog &log);
+void marks_apply(const CaptureLog &log);
 // the captured call on stream s would wait for b's event: record the wait in the log of the
 // capture s belongs to (false if s is not in a capture opened by capture_open)
 bool defer_event_wait(Buffer *b, hipStream_t s);
@@ -130,6 +151,7 @@ struct Plan {
     DeviceArrays mem;
     uint64_t serial = 0;  // track_object (fct_adf_h's internal-edge marker refers to a plan)
     long long int_cells = 0;  // edge cells of the block-internal edges p1v limits
+    int num_kernels = 10;     // stepwise phase 1 stops after this many reference steps
     bool has_ring = false;
     int lmax_edges = 0;
     std::vector<int> owner_cum;  // [n_owned + 1]: edges owned by processing positions < k
@@ -161,11 +183,12 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                      bool with_ring);
 void drop_plans_of(const Buffer *b);
 // fct_adf_h's internal-edge marker (Buffer::int_plan): set after a p1v launch that limited the
-// block-internal edges of `plan` (nullptr clears)
-void mark_internal(Buffer *adf_h, const Plan *plan);
-inline bool has_internal(const Buffer *adf_h) { return adf_h->int_plan != nullptr; }
+// block-internal edges of `plan` (nullptr clears).  `s` is the stream of the call (nullptr for the
+// synchronous uploads): on a captured stream the access is recorded in the capture's log.
+void mark_internal(Buffer *adf_h, const Plan *plan, hipStream_t s);
+bool has_internal(Buffer *adf_h, hipStream_t s);
 // the marked plan if it is still alive (the mark stays)
-const Plan *peek_internal(const Buffer *adf_h);
+const Plan *peek_internal(Buffer *adf_h, hipStream_t s);
 
 // ---- halo exchange (halo_rccl.hip): enqueue pack -> grouped ncclSend/ncclRecv -> unpack on the
 // halo plan's communication stream after the work already queued on `s`.  Returns an event that

@@ -5,8 +5,30 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+
+// The tuning build (make tuning -> lib/libfesom2-accelerate-tuning.so, F2A_TUNING=1) adds the
+// measured-and-rejected kernel variants (fct_ale_variants.hip) and reads the FESOM2_* A/B knobs
+// tools/sweep_env.sh sweeps.  The product library compiles every knob to its measured default:
+// no environment variable changes its kernel selection (the plan options of get_plan aside,
+// which are read once when a mesh plan is built; INTEGRATION.md lists them).
+#ifndef F2A_TUNING
+#define F2A_TUNING 0
+#endif
 
 namespace f2a {
+
+// A/B knob: the environment in the tuning build, the default in the product library.
+static inline int knob(const char *name, int dflt)
+{
+#if F2A_TUNING
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
 
 using real = double;
 

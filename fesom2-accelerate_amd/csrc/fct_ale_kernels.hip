@@ -724,112 +724,6 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
-// Phase 2, horizontal half with b3-horizontal folded in (FESOM2_P2H_FUSE): c-horizontal over the
-// node's edges with each raw fct_adf_h limited in-thread from both endpoints' plus/minus, so the
-// separate b3h pass (read + write of fct_adf_h, plus/minus gathers) and p2h's re-read of the limited
-// flux become one read of the raw flux per endpoint.  The limited flux is stored in place once, by
-// the endpoint that reads the raw flux last: after the block barrier (all raw reads of the block
-// done) one thread per (column, edge) bumps the edge's arrival counter -- counters only ever grow by
-// the edge's owned endpoints, two per pass, so an odd old value marks the second arriver and no
-// reset is needed -- and a halo endpoint never arrives, so the owned one writes.  The writer loads
-// the raw flux and the other endpoint's plus/minus again (L2-resident: its block just read them).
-template <int C, int KB, bool NT, bool ODD>
-__global__ __launch_bounds__(1024) void k_p2hf(MeshPlanDev mp, P2Args a, int G, float invS)
-{
-    extern __shared__ real lds[];  // NodeRec[G] | writer masks[G]
-    const int L = a.nl - 1, S = (L + C - 1) / C;
-    int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
-    if (tr) {
-        a.plus += tr * a.tr.node;
-        a.minus += tr * a.tr.node;
-        a.del_h += tr * a.tr.node;
-        a.adf_h += tr * a.tr.edge;
-        a.edge_cnt += (size_t)tr * mp.n_edges;
-    }
-    unsigned *wmask = reinterpret_cast<unsigned *>(reinterpret_cast<NodeRec *>(lds) + G);
-    if ((int)threadIdx.x < G) wmask[threadIdx.x] = 0u;
-    const int ncol = min(G, a.count - first);
-    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);  // (its barrier also orders wmask)
-    int j, u;
-    slot_of(threadIdx.x, S, invS, j, u);
-    const int z0 = C * u;
-    const bool last1 = ODD && z0 + 1 == L;
-    const bool col = j < ncol;
-    NodeInfo ni{};
-    if (col) ni = recs[j].info;
-    const int nw = col ? max(0, min(C, ni.Ln - z0)) : 0;
-    const int ne = col ? ni.e1 - ni.e0 : 0;
-    real pn[C], mn[C], dh[C];
-    size_t b = 0;
-    if (nw > 0) {
-        b = (size_t)ni.n * L + z0;
-        const size_t ab = (size_t)ni.n * a.nl + z0;
-        ldo<C, ODD>(a.plus + b, pn, last1);
-        ldo<C, ODD>(a.minus + b, mn, last1);
-        ldo_s<C, NT, ODD>(a.del_h + b, dh, last1);
-        real dta[C];
-        if constexpr (C == 2) {  // area: one 16-B load at 8-B alignment (ld_nl)
-            const f2a_d2u t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2a_d2u *>(a.area + ab))
-                                 : *reinterpret_cast<const f2a_d2u *>(a.area + ab);
-            dta[0] = a.dt / t.x;
-            dta[1] = nw >= 2 ? a.dt / t.y : 0.;
-        } else {
-#pragma unroll
-            for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
-        }
-        auto add = [&](int c, real h, int second, int) {
-            dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
-        };
-        for_edges_limited<C, KB, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L,
-                                      add, last1);
-        if (ne > kRecEdge)
-            for_edges_limited<C, KB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.plus, a.minus, pn, mn, z0, L,
-                                          add, last1);
-    }
-    __syncthreads();  // every raw fct_adf_h read of the block is done
-    const int abl = c_ablate;  // timing-only experiments: 16 static writer (racy), 32 no writer
-    for (int k = u; k < ne; k += S) {
-        const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
-        if ((abl & 16) ? !(er.code & 1)
-                       : (er.other >= a.n_owned || (atomicAdd(reinterpret_cast<unsigned *>(a.edge_cnt) + er.edge, 1u) & 1u)))
-            atomicOr(&wmask[j], 1u << k);
-    }
-    __syncthreads();
-    if (nw <= 0) return;
-    stv_s<C, NT>(a.del_h + b, dh, nw);
-    unsigned mine = (abl & 32) ? 0u : wmask[j];
-    while (mine) {  // the edges this column writes, KB at a time
-        int ks[KB];
-#pragma unroll
-        for (int q = 0; q < KB; q++) {
-            ks[q] = mine ? __builtin_ctz(mine) : -1;
-            if (mine) mine &= mine - 1;
-        }
-        EdgeRef er[KB];
-        real h[KB][C], po[KB][C], mo[KB][C];
-#pragma unroll
-        for (int q = 0; q < KB; q++) {
-            er[q] = ks[q] < 0 ? EdgeRef{0, 0, 0} : (ks[q] < kRecEdge ? recs[j].edge[ks[q]] : mp.p_edges[ni.e0 + ks[q]]);
-            if (z0 < (er[q].code >> 1)) {
-                ldo_s<C, NT, ODD>(a.adf_h + (size_t)er[q].edge * L + z0, h[q], last1);
-                ldo<C, ODD>(a.plus + (size_t)er[q].other * L + z0, po[q], last1);
-                ldo<C, ODD>(a.minus + (size_t)er[q].other * L + z0, mo[q], last1);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < KB; q++) {
-            const int lev = er[q].code >> 1, second = er[q].code & 1;
-            if (z0 >= lev) continue;
-            real out[C];
-#pragma unroll
-            for (int c = 0; c < C; c++)
-                out[c] = (second ? b3h_factor(h[q][c], po[q][c], mo[q][c], pn[c], mn[c])
-                                 : b3h_factor(h[q][c], pn[c], mn[c], po[q][c], mo[q][c])) * h[q][c];
-            stv_s<C, NT>(a.adf_h + (size_t)er[q].edge * L + z0, out, min(C, lev - z0));
-        }
-    }
-}
 
 // Phase 2, edges: b3-horizontal (docs/refactoring.md:237-263) in place, G edge columns per block.
 template <int C>
@@ -965,62 +859,6 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
 }
 
 
-// b3-horizontal, node-centric: column j of the block is processing position k and limits the edges
-// k owns (first visited endpoint, MeshPlanDev::p_edge_owner[p_owner_cum[k] ..)), all incident to
-// its node n: n's plus/minus are loaded once, per edge only fct_adf_h (non-temporal) and the other
-// endpoint's plus/minus -- 3 loads per edge instead of 5.  Every edge is written once, by its
-// owner, and read by nobody else in the launch.  Same b3h_factor arithmetic as k_b3h_u.
-template <int C, int EB, bool NT, bool ODD>
-__global__ __launch_bounds__(1024) void k_b3h_n(const NodeInfo *__restrict__ info, const int *__restrict__ owner_cum,
-                                                const int4 *__restrict__ eown, int n_pos, int L, int G, float invS,
-                                                const real *__restrict__ plus, const real *__restrict__ minus,
-                                                real *__restrict__ adf_h, Tracers trs)
-{
-    int tr;
-    const int first = group_tracer(trs.n, tr, c_tracer_major & 2) * G;
-    plus += tr * trs.node;
-    minus += tr * trs.node;
-    adf_h += tr * trs.edge;
-    int j, u;
-    slot_of(threadIdx.x, (L + C - 1) / C, invS, j, u);
-    const int k = first + j;
-    if (j >= G || k >= n_pos) return;
-    const int z0 = C * u;
-    const bool last1 = ODD && z0 + 1 == L;
-    const int e0 = owner_cum[k], e1 = owner_cum[k + 1];
-    if (e0 >= e1) return;
-    const int n = info[k].n;
-    real po[C], mo[C];
-    ldo<C, ODD>(plus + (size_t)n * L + z0, po, last1);
-    ldo<C, ODD>(minus + (size_t)n * L + z0, mo, last1);
-    for (int q0 = e0; q0 < e1; q0 += EB) {
-        int4 ei[EB];
-#pragma unroll
-        for (int q = 0; q < EB; q++) ei[q] = q0 + q < e1 ? eown[q0 + q] : make_int4(0, 0, 0, 0);
-        real f[EB][C], px[EB][C], mx[EB][C];
-#pragma unroll
-        for (int q = 0; q < EB; q++) {
-            if (z0 < ei[q].z) {
-                const int o = ei[q].x == n ? ei[q].y : ei[q].x;
-                ldo_s<C, NT, ODD>(adf_h + (size_t)ei[q].w * L + z0, f[q], last1);
-                ldo<C, ODD>(plus + (size_t)o * L + z0, px[q], last1);
-                ldo<C, ODD>(minus + (size_t)o * L + z0, mx[q], last1);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < EB; q++) {
-            const int nw = min(C, ei[q].z - z0);
-            if (nw <= 0) continue;
-            const bool own_first = ei[q].x == n;  // node1 of the edge (docs/refactoring.md:246-257)
-            real out[C];
-#pragma unroll
-            for (int c = 0; c < C; c++)
-                out[c] = (own_first ? b3h_factor(f[q][c], po[c], mo[c], px[q][c], mx[q][c])
-                                    : b3h_factor(f[q][c], px[q][c], mx[q][c], po[c], mo[c])) * f[q][c];
-            stv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, out, nw);
-        }
-    }
-}
 
 // ============================================================================ reference-sequence
 // entries on the fused path: fct_ale_inter_comm_acc_ (b3v) and fct_ale_c_acc_ (cv + ch) with the
@@ -1299,12 +1137,9 @@ int group_columns(int S)
         }
         if (waste < 1.0 + 1e-9) break;
     }
-    // FESOM2_GROUP_SHIFT = k: 2^k times as many columns per block (k < 0: fewer; A/B measurements,
-    // results do not depend on it)
-    static const int shift = [] {
-        const char *e = getenv("FESOM2_GROUP_SHIFT");
-        return e ? atoi(e) : 0;
-    }();
+    // FESOM2_GROUP_SHIFT = k (tuning build): 2^k times as many columns per block (k < 0: fewer;
+    // A/B measurements, results do not depend on it)
+    static const int shift = knob("FESOM2_GROUP_SHIFT", 0);
     for (int k = 0; k < shift && best * 2 * S <= 1024; k++) best *= 2;
     for (int k = 0; k > shift && best > 1; k--) best /= 2;
     return best;
@@ -1440,15 +1275,19 @@ hipError_t launch_ch(const MeshPlanDev &mp, int nl, const real *adf_h, const rea
 // L <= 1024 levels (one block per column at most); checked by the host entry points.
 
 
+// The launchers below pick the production form of each kernel.  The forms that lost the A/B
+// measurements of DESIGN.md §3 (other gather batches, load placements, cache policies, block
+// shapes) are compiled into the tuning build only (F2A_TUNING, selected by FESOM2_* knobs there).
+
+#if F2A_TUNING
 template <int C, int RB, int EB>
-static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, int G, int S, long groups)
+static hipError_t p1_launch_tuning(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, int G, int S, long groups)
 {
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, a.nl - 1, a.vlimit, false);
-    const bool NT = (env_int("FESOM2_NT", 6) & 1) != 0;
+    const bool NT = (knob("FESOM2_NT", 6) & 1) != 0;
     if constexpr (C == 2 && RB == 2 && EB == 2) {
-        // FESOM2_NL_PAIR: fct_adf_v / area_inv as 16-byte pairs at 8-byte alignment (ld_nl), as p1v
-        if (env_int("FESOM2_NL_PAIR", 1)) {
+        if (knob("FESOM2_NL_PAIR", 1)) {
             if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
             if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
             if (NT) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1460,6 +1299,7 @@ static hipError_t p1_launch(const MeshPlanDev &mp, const P1Args &a, hipStream_t 
     if (NT) F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, true>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p1<1, C, RB, EB, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
+#endif
 
 int fused_group_columns(int nl)
 {
@@ -1467,13 +1307,9 @@ int fused_group_columns(int nl)
     return group_columns(L / levels_per_thread(L));
 }
 
-// odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0: one level
-// per thread)
-static bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && env_int("FESOM2_ODD_PAIR", 1) != 0; }
-
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
-    if (odd_pairs(a.nl - 1) && a.vlimit == 1 && !env_int("FESOM2_P1_EDGE", 0) && !env_int("FESOM2_P1_STAGE", 0)) {
+    if (odd_pairs(a.nl - 1) && a.vlimit == 1 && !knob("FESOM2_P1_EDGE", 0) && !knob("FESOM2_P1_STAGE", 0)) {
         const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
@@ -1481,18 +1317,32 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     }
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-    // opt-in phase-1 variants (fct_ale_variants.hip)
+#if F2A_TUNING
+    // opt-in phase-1 variants (fct_ale_variants.hip), other gather batches (FESOM2_P1_BATCH =
+    // 10*RB + EB), cache policies
     bool handled = false;
     const hipError_t ve = launch_p1_variant(mp, a, s, &handled);
     if (handled) return ve;
-    // batch sizes of the cluster / edge gathers (FESOM2_P1_BATCH = 10*RB + EB; measured)
-    switch (env_int("FESOM2_P1_BATCH", 22)) {
-    case 44: return C == 2 ? p1_launch<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch<1, 4, 4>(mp, a, s, G, S, groups);
-    case 24: return C == 2 ? p1_launch<2, 2, 4>(mp, a, s, G, S, groups) : p1_launch<1, 2, 4>(mp, a, s, G, S, groups);
-    case 42: return C == 2 ? p1_launch<2, 4, 2>(mp, a, s, G, S, groups) : p1_launch<1, 4, 2>(mp, a, s, G, S, groups);
-    case 88: return C == 2 ? p1_launch<2, 8, 8>(mp, a, s, G, S, groups) : p1_launch<1, 8, 8>(mp, a, s, G, S, groups);
-    default: return C == 2 ? p1_launch<2, 2, 2>(mp, a, s, G, S, groups) : p1_launch<1, 2, 2>(mp, a, s, G, S, groups);
+    switch (knob("FESOM2_P1_BATCH", 22)) {
+    case 44: return C == 2 ? p1_launch_tuning<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 4, 4>(mp, a, s, G, S, groups);
+    case 24: return C == 2 ? p1_launch_tuning<2, 2, 4>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 2, 4>(mp, a, s, G, S, groups);
+    case 42: return C == 2 ? p1_launch_tuning<2, 4, 2>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 4, 2>(mp, a, s, G, S, groups);
+    case 88: return C == 2 ? p1_launch_tuning<2, 8, 8>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 8, 8>(mp, a, s, G, S, groups);
+    default: return C == 2 ? p1_launch_tuning<2, 2, 2>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 2, 2>(mp, a, s, G, S, groups);
     }
+#else
+    // gathers in batches of 2 (58 VGPRs, 8 waves/SIMD), 16-byte pairs of the stride-nl arrays
+    const float invS = 1.0f / (float)S;
+    const size_t lds = p1_lds_bytes(G, L, a.vlimit, false);
+    if (C == 2) {
+        if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, false, 4>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
+    if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
+#endif
 }
 
 int p1v_group_columns(int nl)
@@ -1510,28 +1360,28 @@ static int p1v_launch_G(int nl, int vlimit)
     return group_columns(L / levels_per_thread(L));
 }
 
-// the launch_p1v forms with the internal-edge tail: vlimit 1, the plan's block size, and the
-// default load placement (FESOM2_P1V_EARLY = 0)
+// the launch_p1v forms with the internal-edge tail: the plan built the lists for this block size
+// (in the tuning build also the default load placement, and no phase-2 variant that limits every
+// edge itself)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 {
-    // (the opt-in phase-2 forms that limit every edge themselves keep all of them)
     return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit >= 1 && a.vlimit <= 3 &&
-           env_int("FESOM2_P1V_B3H", 1) != 0 && env_int("FESOM2_P1V_EARLY", 0) == 0 && !env_int("FESOM2_P2H_FUSE", 0) &&
-           !env_int("FESOM2_B3H_NODE", 0) && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
+           knob("FESOM2_P1V_B3H", 1) != 0 && knob("FESOM2_P1V_EARLY", 0) == 0 && !knob("FESOM2_P2H_FUSE", 0) &&
+           !knob("FESOM2_B3H_NODE", 0) && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
 }
 
-hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
+#if F2A_TUNING
+// every measured form of p1v (FESOM2_NT bit 2, FESOM2_P1V_EARLY, FESOM2_NL_PAIR, FESOM2_P1V_INT_DMA)
+static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in)
 {
     const int L = a.nl - 1;
-    const bool in = p1v_limits_internal(mp, a);
     if (odd_pairs(L) && a.vlimit == 1) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, 1, in);
-        if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
         const float inv = 1.0f / (float)S;
-        if ((env_int("FESOM2_NT", 6) & 4) != 0) {  // non-temporal single-use streams (see below)
-            if (in && env_int("FESOM2_P1V_INT_DMA", 1))  // internal-edge entries staged by DMA (OPT & 32)
+        if ((knob("FESOM2_NT", 6) & 4) != 0) {
+            if (in && knob("FESOM2_P1V_INT_DMA", 1))
                 F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv);
             if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
@@ -1543,15 +1393,12 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
-    if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
     // OPT bits of k_p1 (VERT): 1 area_inv issued with the first loads, 2 + the tail's own streams
     // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default),
-    // 16 the block-internal edges' b3-horizontal (p1v_limits_internal)
-    const int early = env_int("FESOM2_P1V_EARLY", 0) | (env_int("FESOM2_NL_PAIR", 1) ? 4 : 0);
-    // FESOM2_NT bit 2: p1v's single-use streams non-temporal (plus/minus/del_v stores, the tail's
-    // del_v/hnode/hnode_new loads; measured -1.5 % per pass; the stride-nl ones stay cached: +1 %)
-    const bool nt = (env_int("FESOM2_NT", 6) & 4) != 0;
-    if (a.vlimit != 1 && C == 2 && early == 4 && nt) {  // vlimit 2/3 in the production shape
+    // 8 the tail's streams staged into LDS by DMA, 16 the block-internal edges' b3-horizontal
+    const int early = knob("FESOM2_P1V_EARLY", 0) | (knob("FESOM2_NL_PAIR", 1) ? 4 : 0);
+    const bool nt = (knob("FESOM2_NT", 6) & 4) != 0;
+    if (a.vlimit != 1 && C == 2 && early == 4 && nt) {
         if (in && a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
         if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1565,7 +1412,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         if (C == 2) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if (in && C == 2 && early == 4 && nt && env_int("FESOM2_P1V_INT_DMA", 1))
+    if (in && C == 2 && early == 4 && nt && knob("FESOM2_P1V_INT_DMA", 1))
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, a, G, invS);
     if (in && C == 2 && early == 4 && nt)
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1590,78 +1437,116 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
 }
+#endif
+
+hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
+{
+    if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
+    const bool in = p1v_limits_internal(mp, a);
+#if F2A_TUNING
+    return launch_p1v_tuning(mp, a, s, in);
+#else
+    const int L = a.nl - 1;
+    // OPT 4: 16-byte loads/stores of the stride-nl arrays; +16 the block-internal edges'
+    // b3-horizontal, +32 their entries staged into LDS by DMA.  NT: the single-use streams
+    // (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
+    if (odd_pairs(L) && a.vlimit == 1) {
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = p1_lds_bytes(G, L, 1, in);
+        const float inv = 1.0f / (float)S;
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+    }
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
+    if (C == 2) {
+        switch (a.vlimit) {
+        case 2:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        case 3:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        default:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
+        }
+    }
+    // one level per thread (odd L at vlimit 2/3, or L < 3)
+    switch (a.vlimit) {
+    case 2:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    case 3:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    default:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 16>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+#endif
+}
 
 hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
     const int L = a.nl - 1;
+    // single-use streams non-temporal (FESOM2_NT bit 1), 16-byte loads of the stride-nl area
+    const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
+    const bool pair = knob("FESOM2_NL_PAIR", 1) != 0;
     if (odd_pairs(L)) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.count + G - 1) / G * a.tr.n;
         const size_t lds = (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
-        if ((env_int("FESOM2_NT", 6) & 2) != 0)
-            F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+#if F2A_TUNING
+        if (!NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+#endif
+        F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
-    const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;
-    const bool pair = env_int("FESOM2_NL_PAIR", 1) != 0;  // 16-B loads of the stride-nl area (ld_nl)
+#if F2A_TUNING
     if (C == 2) {
-        if (NT && pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true>), groups, G, S, lds, s, mp, a, G, invS);
-        if (NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
-        if (pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2h<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (NT && !pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (!NT && pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (!NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if (NT) F2A_LAUNCH_GROUPS((k_p2h<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p2h<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
-}
-
-hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
-{
-    const int L = a.nl - 1;
-    const bool odd = odd_pairs(L);
-    const int C = odd ? 2 : levels_per_thread(L), S = (L + C - 1) / C, G = group_columns(S);
-    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
-    const float invS = 1.0f / (float)S;
-    const size_t lds = (size_t)G * sizeof(NodeRec) + G * sizeof(unsigned);
-    const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;
-    const int KB = env_int("FESOM2_P2HF_KB", 2);
-    if (odd) {
-        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, true>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
-    }
-    if (C == 2) {
-        if (KB == 4) F2A_LAUNCH_GROUPS((k_p2hf<2, 4, true, false>), groups, G, S, lds, s, mp, a, G, invS);
-        if (KB == 1) F2A_LAUNCH_GROUPS((k_p2hf<2, 1, true, false>), groups, G, S, lds, s, mp, a, G, invS);
-        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, false>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
-    }
-    F2A_LAUNCH_GROUPS((k_p2hf<1, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
+    if (!NT) F2A_LAUNCH_GROUPS((k_p2h<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+#else
+    (void)NT, (void)pair;
+#endif
+    if (C == 2) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2h<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 {
     const int L = a.nl - 1;
-    // levels per thread of the node kernel: FESOM2_P2_CPT (1 or 2; default as the other kernels)
-    const int C = (L % 2 == 0 && env_int("FESOM2_P2_CPT", levels_per_thread(L)) == 2) ? 2 : 1;
+    // levels per thread of the node kernel: FESOM2_P2_CPT (tuning build; default as the other kernels)
+    const int C = (L % 2 == 0 && knob("FESOM2_P2_CPT", levels_per_thread(L)) == 2) ? 2 : 1;
     const int S = L / C, G = group_columns(S);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
-    const int KB = env_int("FESOM2_P2_BATCH", 4);
     const size_t lds = (size_t)G * sizeof(NodeRec);
-    if (C == 2) {
-        const bool NT = (env_int("FESOM2_NT", 6) & 2) != 0;  // measured: p2 streams non-temporal (-2 %)
-        if (NT) F2A_LAUNCH_GROUPS((k_p2<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
-        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
-        F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+#if F2A_TUNING
+    const int KB = knob("FESOM2_P2_BATCH", 4);
+    const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
+    if (!NT || KB != 4) {
+        if (C == 2 && KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (C == 2) F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    if ((env_int("FESOM2_NT", 6) & 2) != 0) F2A_LAUNCH_GROUPS((k_p2<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
-    if (KB == 8) F2A_LAUNCH_GROUPS((k_p2<1, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
-    if (KB == 2) F2A_LAUNCH_GROUPS((k_p2<1, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
-    F2A_LAUNCH_GROUPS((k_p2<1, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
+#endif
+    // edge gathers in batches of 4, single-use streams non-temporal (measured -2 %)
+    if (C == 2) F2A_LAUNCH_GROUPS((k_p2<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
+    F2A_LAUNCH_GROUPS((k_p2<1, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
 hipError_t launch_b3v_cols(int n_owned, int nl, const int *nlev, const real *plus, const real *minus, real *adf_v,
@@ -1690,77 +1575,55 @@ hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     F2A_LAUNCH_GROUPS((k_c<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
 
-hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
-                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
-{
-    const int L = nl - 1, N = mp.n_owned;
-    if (!mp.p_owner_cum || !mp.node_info) return hipErrorInvalidValue;
-    const bool odd = L % 2 == 1;
-    const int C = (L % 2 == 0 || odd_pairs(L)) ? 2 : 1;
-    const int S = (L + C - 1) / C, G = group_columns(S);
-    const long groups = (long)(N + G - 1) / G * tr.n;
-    const float invS = 1.0f / (float)S;
-    const int EB = env_int("FESOM2_B3HN_EB", 2);
-    auto go = [&]() -> hipError_t {
-        if (C == 2 && !odd) {
-            if (EB == 1) F2A_LAUNCH_GROUPS((k_b3h_n<2, 1, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
-                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
-            if (EB == 3) F2A_LAUNCH_GROUPS((k_b3h_n<2, 3, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
-                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
-            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
-                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
-        }
-        if (C == 2)
-            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, true>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
-                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
-        F2A_LAUNCH_GROUPS((k_b3h_n<1, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
-                          mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
-    };
-    const hipError_t e = go();
-    if (e != hipSuccess || owned_edges >= n_edges) return e;
-    // edges without an owned endpoint (none in a FESOM partition): edge-centric
-    return launch_b3h_edges(mp.p_edge_owner + owned_edges, n_edges - owned_edges, nl, plus, minus, adf_h, tr, s);
-}
-
-// packed b3h over descriptors [d0, d1) of a list (k_b3h_p), or false if packing is off for this L
+// packed b3h over descriptors [d0, d1) of a list (k_b3h_p), or false if packing is off for this L.
+// Production form: two level-pair slots per thread, fct_adf_h non-temporal, and on a regular list
+// (reg.x > 0: every edge the same slot count) no descriptor loads.
 static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const int4 *einfo, int cap, int d0, int d1,
                               int nl, const real *plus, const real *minus, real *adf_h, const Tracers &tr,
                               hipStream_t s, hipError_t *err, int4 reg = make_int4(0, 0, 0, 0))
 {
     const int L = nl - 1;
-    if (!desc || !env_int("FESOM2_B3H_PACK", 1) || !(L % 2 == 0 || odd_pairs(L))) return false;
+    if (!desc || !knob("FESOM2_B3H_PACK", 1) || !(L % 2 == 0 || odd_pairs(L))) return false;
     const long groups = (long)(d1 - d0) * tr.n;
-    const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
     init_swizzle();
     *err = hipSuccess;
     if (groups <= 0) return true;
-    // slots per thread; the 1- and 4-slot forms exist for even L with non-temporal streams only,
-    // and the block must cover the capacity for the form actually launched
-    int H = env_int("FESOM2_B3HP_H", 2);
-    if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
-    const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
     const int4 none = make_int4(0, 0, 0, 0);
-    // regular list (reg.x > 0: every edge the same slot count): no descriptor loads (FESOM2_B3HP_REG)
-    if (reg.x > 0 && H == 2 && NT && env_int("FESOM2_B3HP_REG", 1)) {
+#if F2A_TUNING
+    // slots per thread (FESOM2_B3HP_H 1 or 4: even L, non-temporal only, the block must cover the
+    // capacity), cached fct_adf_h (FESOM2_B3H_NT=0), descriptor loads on regular lists (FESOM2_B3HP_REG=0)
+    const bool NT = knob("FESOM2_B3H_NT", 1) != 0;
+    int H = knob("FESOM2_B3HP_H", 2);
+    if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
+    if (H != 2 || !NT || !knob("FESOM2_B3HP_REG", 1)) {
+        const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
+        if (H == 1)
+            hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        else if (H == 4)
+            hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        else if (L % 2)
+            hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        else if (NT)
+            hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        else
+            hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        *err = hipGetLastError();
+        return true;
+    }
+#endif
+    const dim3 grid((unsigned)groups), block((cap + 1) / 2);
+    if (reg.x > 0) {
         if (L % 2)
             hipLaunchKernelGGL((k_b3h_p<true, true, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
                                adf_h, tr, reg);
         else
             hipLaunchKernelGGL((k_b3h_p<true, false, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
                                adf_h, tr, reg);
-        *err = hipGetLastError();
-        return true;
-    }
-    if (H == 1)
-        hipLaunchKernelGGL((k_b3h_p<true, false, 1>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
-    else if (H == 4)
-        hipLaunchKernelGGL((k_b3h_p<true, false, 4>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
-    else if (L % 2)
+    } else if (L % 2) {
         hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
-    else if (NT)
+    } else {
         hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
-    else
-        hipLaunchKernelGGL((k_b3h_p<false, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+    }
     *err = hipGetLastError();
     return true;
 }
@@ -1768,7 +1631,7 @@ static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
 {
-    // packed by depth (FESOM2_B3H_PACK=1): the plan's descriptors for exactly these edge ranges
+    // packed by depth: the plan's descriptors for exactly these edge ranges
     int d0 = -1, d1 = -1, sl = 0;  // sl: regular slot count of the edge range, if any
     const int ni = mp.n_edge_interior;
     if (begin == 0 && count == mp.n_edges) d0 = 0, d1 = mp.b3p_ndesc, sl = ni == mp.n_edges ? mp.b3p_slots_int : 0;
@@ -1797,53 +1660,47 @@ hipError_t launch_b3h_ext(const MeshPlanDev &mp, int nl, const real *plus, const
     return launch_b3h_edges(mp.p_edge_ext, mp.n_ext_interior, nl, plus, minus, adf_h, tr, s);
 }
 
+// b3-horizontal over an explicit edge list: two edge groups per block (every einfo load, then every
+// data load of both groups issued before use), fct_adf_h non-temporal
 hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus, const real *minus,
                             real *adf_h, const Tracers &tr, hipStream_t s)
 {
     const int L = nl - 1;
     if (odd_pairs(L)) {
         const int S = (L + 1) / 2, G = group_columns(S);
-        const long ug = ((count + G - 1) / G + 1) / 2 * tr.n;  // two edge groups per block
+        const long ug = ((count + G - 1) / G + 1) / 2 * tr.n;
         F2A_LAUNCH_GROUPS((k_b3h_u<2, 2, true, true>), ug, G, S, 0, s, ei, count, L, G, 1.0f / (float)S, plus, minus,
                           adf_h, tr);
     }
     int C = levels_per_thread(L);
-    if (C == 2 && L % 4 == 0 && env_int("FESOM2_B3H_CPT", 2) == 4) C = 4;  // 4 levels: 2 x 16 B per array
-    const int S = L / C, G = group_columns(S);
-    const long groups = (count + G - 1) / G;
-    const float invS = 1.0f / (float)S;
-    const long tg = groups * tr.n;
-    if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
-    if (C == 2) {
-        // U edge groups per block, fct_adf_h non-temporal (FESOM2_B3H_U / FESOM2_B3H_NT; measured)
-        const int U = env_int("FESOM2_B3H_U", 2);
-        const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
-        const long ug = (groups + U - 1) / U * tr.n;
-#define F2A_B3H_U(UU)                                                                                   \
-        if (U == UU) {                                                                                  \
-            if (NT) F2A_LAUNCH_GROUPS((k_b3h_u<2, UU, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr); \
-            F2A_LAUNCH_GROUPS((k_b3h_u<2, UU, false>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr); \
-        }
-        F2A_B3H_U(2)
-        F2A_B3H_U(4)
-        F2A_B3H_U(8)
-#undef F2A_B3H_U
-        if (NT) F2A_LAUNCH_GROUPS((k_b3h_u<2, 1, true>), tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
-        F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
-    }
-    {
-        // one level per thread (odd L): the same two-groups-per-block, non-temporal form
-        const int U = env_int("FESOM2_B3H_U", 2);
-        const bool NT = env_int("FESOM2_B3H_NT", 1) != 0;
-        const long ug = (groups + U - 1) / U * tr.n;
-        if (U == 2 && NT) F2A_LAUNCH_GROUPS((k_b3h_u<1, 2, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+    const int S0 = L / C, G0 = group_columns(S0);
+    const long groups0 = (count + G0 - 1) / G0;
+#if F2A_TUNING
+    // 4 levels per thread (FESOM2_B3H_CPT=4), U edge groups per block (FESOM2_B3H_U), cached
+    // fct_adf_h (FESOM2_B3H_NT=0)
+    if (C == 2 && L % 4 == 0 && knob("FESOM2_B3H_CPT", 2) == 4) C = 4;
+    const int U = knob("FESOM2_B3H_U", 2);
+    const bool NT = knob("FESOM2_B3H_NT", 1) != 0;
+    if (C == 4 || U != 2 || !NT) {
+        const int S = L / C, G = group_columns(S);
+        const long groups = (count + G - 1) / G;
+        const float invS = 1.0f / (float)S;
+        const long tg = groups * tr.n, ug = (groups + U - 1) / U * tr.n;
+        if (C == 4) F2A_LAUNCH_GROUPS(k_b3h_g<4>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (C == 2 && NT && U == 4) F2A_LAUNCH_GROUPS((k_b3h_u<2, 4, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (C == 2 && NT && U == 8) F2A_LAUNCH_GROUPS((k_b3h_u<2, 8, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (C == 2 && NT && U == 1) F2A_LAUNCH_GROUPS((k_b3h_u<2, 1, true>), tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (C == 2 && !NT && U == 2) F2A_LAUNCH_GROUPS((k_b3h_u<2, 2, false>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        if (C == 2) F2A_LAUNCH_GROUPS(k_b3h_g<2>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
         if (U == 4 && NT) F2A_LAUNCH_GROUPS((k_b3h_u<1, 4, true>), ug, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+        F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
     }
-    F2A_LAUNCH_GROUPS(k_b3h_g<1>, tg, G, S, 0, s, ei, count, L, G, invS, plus, minus, adf_h, tr);
+#endif
+    const float invS = 1.0f / (float)S0;
+    const long ug = (groups0 + 1) / 2 * tr.n;
+    if (C == 2) F2A_LAUNCH_GROUPS((k_b3h_u<2, 2, true>), ug, G0, S0, 0, s, ei, count, L, G0, invS, plus, minus, adf_h, tr);
+    F2A_LAUNCH_GROUPS((k_b3h_u<1, 2, true>), ug, G0, S0, 0, s, ei, count, L, G0, invS, plus, minus, adf_h, tr);
 }
-
-
-
 
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)
 {

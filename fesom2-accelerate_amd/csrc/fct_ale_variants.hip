@@ -5,9 +5,235 @@
 //   * k_p2f  FESOM2_FUSE_B3H=1  b3-horizontal folded into the node kernel (arrival counters)
 //   * k_p2_b3h_chunk  FESOM2_P2_CHUNK + FESOM2_P2_MERGE  chunked phase 2, merged boundaries
 //   * k_p2w  FESOM2_P2_WF=1     phase 2 as one persistent launch with per-tile hand-offs
+//   * k_p2hf FESOM2_P2H_FUSE=1  b3-horizontal folded into c-horizontal on the split pass
+//   * k_b3h_n FESOM2_B3H_NODE=1 b3-horizontal node-centric over the owner order
+// Compiled into the tuning build only (make tuning, F2A_TUNING=1); the product library has none.
 #include "f2a_device.hpp"
 
+#if !F2A_TUNING
+#error "fct_ale_variants.hip belongs to the tuning build (make tuning)"
+#endif
+
 namespace f2a {
+
+// Phase 2, horizontal half with b3-horizontal folded in (FESOM2_P2H_FUSE): c-horizontal over the
+// node's edges with each raw fct_adf_h limited in-thread from both endpoints' plus/minus, so the
+// separate b3h pass (read + write of fct_adf_h, plus/minus gathers) and p2h's re-read of the limited
+// flux become one read of the raw flux per endpoint.  The limited flux is stored in place once, by
+// the endpoint that reads the raw flux last: after the block barrier (all raw reads of the block
+// done) one thread per (column, edge) bumps the edge's arrival counter -- counters only ever grow by
+// the edge's owned endpoints, two per pass, so an odd old value marks the second arriver and no
+// reset is needed -- and a halo endpoint never arrives, so the owned one writes.  The writer loads
+// the raw flux and the other endpoint's plus/minus again (L2-resident: its block just read them).
+template <int C, int KB, bool NT, bool ODD>
+__global__ __launch_bounds__(1024) void k_p2hf(MeshPlanDev mp, P2Args a, int G, float invS)
+{
+    extern __shared__ real lds[];  // NodeRec[G] | writer masks[G]
+    const int L = a.nl - 1, S = (L + C - 1) / C;
+    int tr;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    if (tr) {
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.del_h += tr * a.tr.node;
+        a.adf_h += tr * a.tr.edge;
+        a.edge_cnt += (size_t)tr * mp.n_edges;
+    }
+    unsigned *wmask = reinterpret_cast<unsigned *>(reinterpret_cast<NodeRec *>(lds) + G);
+    if ((int)threadIdx.x < G) wmask[threadIdx.x] = 0u;
+    const int ncol = min(G, a.count - first);
+    const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);  // (its barrier also orders wmask)
+    int j, u;
+    slot_of(threadIdx.x, S, invS, j, u);
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    const bool col = j < ncol;
+    NodeInfo ni{};
+    if (col) ni = recs[j].info;
+    const int nw = col ? max(0, min(C, ni.Ln - z0)) : 0;
+    const int ne = col ? ni.e1 - ni.e0 : 0;
+    real pn[C], mn[C], dh[C];
+    size_t b = 0;
+    if (nw > 0) {
+        b = (size_t)ni.n * L + z0;
+        const size_t ab = (size_t)ni.n * a.nl + z0;
+        ldo<C, ODD>(a.plus + b, pn, last1);
+        ldo<C, ODD>(a.minus + b, mn, last1);
+        ldo_s<C, NT, ODD>(a.del_h + b, dh, last1);
+        real dta[C];
+        if constexpr (C == 2) {  // area: one 16-B load at 8-B alignment (ld_nl)
+            const f2a_d2u t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2a_d2u *>(a.area + ab))
+                                 : *reinterpret_cast<const f2a_d2u *>(a.area + ab);
+            dta[0] = a.dt / t.x;
+            dta[1] = nw >= 2 ? a.dt / t.y : 0.;
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; c++) dta[c] = c < nw ? a.dt / ld1_s<NT>(a.area + ab + c) : 0.;
+        }
+        auto add = [&](int c, real h, int second, int) {
+            dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
+        };
+        for_edges_limited<C, KB, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                      add, last1);
+        if (ne > kRecEdge)
+            for_edges_limited<C, KB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, a.plus, a.minus, pn, mn, z0, L,
+                                          add, last1);
+    }
+    __syncthreads();  // every raw fct_adf_h read of the block is done
+    const int abl = c_ablate;  // timing-only experiments: 16 static writer (racy), 32 no writer
+    for (int k = u; k < ne; k += S) {
+        const EdgeRef er = k < kRecEdge ? recs[j].edge[k] : mp.p_edges[ni.e0 + k];
+        if ((abl & 16) ? !(er.code & 1)
+                       : (er.other >= a.n_owned || (atomicAdd(reinterpret_cast<unsigned *>(a.edge_cnt) + er.edge, 1u) & 1u)))
+            atomicOr(&wmask[j], 1u << k);
+    }
+    __syncthreads();
+    if (nw <= 0) return;
+    stv_s<C, NT>(a.del_h + b, dh, nw);
+    unsigned mine = (abl & 32) ? 0u : wmask[j];
+    while (mine) {  // the edges this column writes, KB at a time
+        int ks[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            ks[q] = mine ? __builtin_ctz(mine) : -1;
+            if (mine) mine &= mine - 1;
+        }
+        EdgeRef er[KB];
+        real h[KB][C], po[KB][C], mo[KB][C];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            er[q] = ks[q] < 0 ? EdgeRef{0, 0, 0} : (ks[q] < kRecEdge ? recs[j].edge[ks[q]] : mp.p_edges[ni.e0 + ks[q]]);
+            if (z0 < (er[q].code >> 1)) {
+                ldo_s<C, NT, ODD>(a.adf_h + (size_t)er[q].edge * L + z0, h[q], last1);
+                ldo<C, ODD>(a.plus + (size_t)er[q].other * L + z0, po[q], last1);
+                ldo<C, ODD>(a.minus + (size_t)er[q].other * L + z0, mo[q], last1);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            const int lev = er[q].code >> 1, second = er[q].code & 1;
+            if (z0 >= lev) continue;
+            real out[C];
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                out[c] = (second ? b3h_factor(h[q][c], po[q][c], mo[q][c], pn[c], mn[c])
+                                 : b3h_factor(h[q][c], pn[c], mn[c], po[q][c], mo[q][c])) * h[q][c];
+            stv_s<C, NT>(a.adf_h + (size_t)er[q].edge * L + z0, out, min(C, lev - z0));
+        }
+    }
+}
+
+// b3-horizontal, node-centric: column j of the block is processing position k and limits the edges
+// k owns (first visited endpoint, MeshPlanDev::p_edge_owner[p_owner_cum[k] ..)), all incident to
+// its node n: n's plus/minus are loaded once, per edge only fct_adf_h (non-temporal) and the other
+// endpoint's plus/minus -- 3 loads per edge instead of 5.  Every edge is written once, by its
+// owner, and read by nobody else in the launch.  Same b3h_factor arithmetic as k_b3h_u.
+template <int C, int EB, bool NT, bool ODD>
+__global__ __launch_bounds__(1024) void k_b3h_n(const NodeInfo *__restrict__ info, const int *__restrict__ owner_cum,
+                                                const int4 *__restrict__ eown, int n_pos, int L, int G, float invS,
+                                                const real *__restrict__ plus, const real *__restrict__ minus,
+                                                real *__restrict__ adf_h, Tracers trs)
+{
+    int tr;
+    const int first = group_tracer(trs.n, tr, c_tracer_major & 2) * G;
+    plus += tr * trs.node;
+    minus += tr * trs.node;
+    adf_h += tr * trs.edge;
+    int j, u;
+    slot_of(threadIdx.x, (L + C - 1) / C, invS, j, u);
+    const int k = first + j;
+    if (j >= G || k >= n_pos) return;
+    const int z0 = C * u;
+    const bool last1 = ODD && z0 + 1 == L;
+    const int e0 = owner_cum[k], e1 = owner_cum[k + 1];
+    if (e0 >= e1) return;
+    const int n = info[k].n;
+    real po[C], mo[C];
+    ldo<C, ODD>(plus + (size_t)n * L + z0, po, last1);
+    ldo<C, ODD>(minus + (size_t)n * L + z0, mo, last1);
+    for (int q0 = e0; q0 < e1; q0 += EB) {
+        int4 ei[EB];
+#pragma unroll
+        for (int q = 0; q < EB; q++) ei[q] = q0 + q < e1 ? eown[q0 + q] : make_int4(0, 0, 0, 0);
+        real f[EB][C], px[EB][C], mx[EB][C];
+#pragma unroll
+        for (int q = 0; q < EB; q++) {
+            if (z0 < ei[q].z) {
+                const int o = ei[q].x == n ? ei[q].y : ei[q].x;
+                ldo_s<C, NT, ODD>(adf_h + (size_t)ei[q].w * L + z0, f[q], last1);
+                ldo<C, ODD>(plus + (size_t)o * L + z0, px[q], last1);
+                ldo<C, ODD>(minus + (size_t)o * L + z0, mx[q], last1);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < EB; q++) {
+            const int nw = min(C, ei[q].z - z0);
+            if (nw <= 0) continue;
+            const bool own_first = ei[q].x == n;  // node1 of the edge (docs/refactoring.md:246-257)
+            real out[C];
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                out[c] = (own_first ? b3h_factor(f[q][c], po[c], mo[c], px[q][c], mx[q][c])
+                                    : b3h_factor(f[q][c], px[q][c], mx[q][c], po[c], mo[c])) * f[q][c];
+            stv_s<C, NT>(adf_h + (size_t)ei[q].w * L + z0, out, nw);
+        }
+    }
+}
+
+hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
+{
+    const int L = a.nl - 1;
+    const bool odd = odd_pairs(L);
+    const int C = odd ? 2 : levels_per_thread(L), S = (L + C - 1) / C, G = group_columns(S);
+    const long groups = (long)(a.count + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = (size_t)G * sizeof(NodeRec) + G * sizeof(unsigned);
+    const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
+    const int KB = knob("FESOM2_P2HF_KB", 2);
+    if (odd) {
+        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    if (C == 2) {
+        if (KB == 4) F2A_LAUNCH_GROUPS((k_p2hf<2, 4, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (KB == 1) F2A_LAUNCH_GROUPS((k_p2hf<2, 1, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        if (NT) F2A_LAUNCH_GROUPS((k_p2hf<2, 2, true, false>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p2hf<2, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+    F2A_LAUNCH_GROUPS((k_p2hf<1, 2, false, false>), groups, G, S, lds, s, mp, a, G, invS);
+}
+hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
+                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s)
+{
+    const int L = nl - 1, N = mp.n_owned;
+    if (!mp.p_owner_cum || !mp.node_info) return hipErrorInvalidValue;
+    const bool odd = L % 2 == 1;
+    const int C = (L % 2 == 0 || odd_pairs(L)) ? 2 : 1;
+    const int S = (L + C - 1) / C, G = group_columns(S);
+    const long groups = (long)(N + G - 1) / G * tr.n;
+    const float invS = 1.0f / (float)S;
+    const int EB = knob("FESOM2_B3HN_EB", 2);
+    auto go = [&]() -> hipError_t {
+        if (C == 2 && !odd) {
+            if (EB == 1) F2A_LAUNCH_GROUPS((k_b3h_n<2, 1, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+            if (EB == 3) F2A_LAUNCH_GROUPS((k_b3h_n<2, 3, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                                           mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+        }
+        if (C == 2)
+            F2A_LAUNCH_GROUPS((k_b3h_n<2, 2, true, true>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                              mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+        F2A_LAUNCH_GROUPS((k_b3h_n<1, 2, true, false>), groups, G, S, 0, s, mp.node_info, mp.p_owner_cum,
+                          mp.p_edge_owner, N, L, G, invS, plus, minus, adf_h, tr);
+    };
+    const hipError_t e = go();
+    if (e != hipSuccess || owned_edges >= n_edges) return e;
+    // edges without an owned endpoint (none in a FESOM partition): edge-centric
+    return launch_b3h_edges(mp.p_edge_owner + owned_edges, n_edges - owned_edges, nl, plus, minus, adf_h, tr, s);
+}
+
 
 // Phase-1 edge loop that also gathers the cluster (MeshPlanDev::edge_cluster): per edge the raw
 // flux and the other endpoint's LO/ttf, kBatch edges at a time; b1-horizontal sums in ascending
@@ -592,10 +818,10 @@ hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     // cluster along the edge list (FESOM2_P1_EDGE=1 where the plan verified it; measured equal at
     // EB = 1, slower at EB >= 2: DESIGN.md §3)
-    if (mp.edge_cluster && env_int("FESOM2_P1_EDGE", 0)) {
+    if (mp.edge_cluster && knob("FESOM2_P1_EDGE", 0)) {
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
-        const int EB = env_int("FESOM2_P1E_EB", 2);
+        const int EB = knob("FESOM2_P1E_EB", 2);
 #define F2A_P1E(CC, EBV)                                                                                        \
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1e<2, CC, EBV>), groups, G, S, lds, s, mp, a, G, invS);  \
         if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1e<3, CC, EBV>), groups, G, S, lds, s, mp, a, G, invS);  \
@@ -610,11 +836,11 @@ hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t
 #undef F2A_P1E
     }
     // staged cluster (FESOM2_P1_STAGE=1; vlimit 1 only; measured slower at G = 8)
-    if (a.vlimit == 1 && mp.stage_max > 0 && mp.stage_G == G && env_int("FESOM2_P1_STAGE", 0)) {
+    if (a.vlimit == 1 && mp.stage_max > 0 && mp.stage_G == G && knob("FESOM2_P1_STAGE", 0)) {
         const int U = std::max(mp.stage_max, G);
         const size_t lds = 2 * (size_t)U * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
-        const int EB = env_int("FESOM2_P1S_EB", 2);
+        const int EB = knob("FESOM2_P1S_EB", 2);
         const int KS = (mp.stage_max * S + (int)threads_for(G, S) - 1) / (int)threads_for(G, S);  // items per thread
         if (C == 2 && KS <= 8) {
 #define F2A_P1S(EBV, KSV) \
@@ -634,7 +860,7 @@ hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * (sizeof(NodeRec) + sizeof(unsigned));
-    const int KB = env_int("FESOM2_P2F_BATCH", 2);
+    const int KB = knob("FESOM2_P2F_BATCH", 2);
     if (C == 2) {
         if (KB == 4) F2A_LAUNCH_GROUPS((k_p2f<2, 4>), groups, G, S, lds, s, mp, a, G, invS);
         if (KB == 1) F2A_LAUNCH_GROUPS((k_p2f<2, 1>), groups, G, S, lds, s, mp, a, G, invS);
@@ -678,7 +904,7 @@ hipError_t launch_p2_wavefront(const MeshPlanDev &mp, const P2Args &a, int *stat
     else
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_p2w<1, 4>, threads, lds);
     long grid = (long)std::max(1, per_cu) * std::max(ncu, 1);
-    if (getenv("FESOM2_PLAN_STATS")) fprintf(stderr, "fesom2-accelerate: wavefront grid %ld (%d per CU)\n", grid, per_cu);
+    if (knob("FESOM2_PLAN_STATS", 0)) fprintf(stderr, "fesom2-accelerate: wavefront grid %ld (%d per CU)\n", grid, per_cu);
     grid = std::max<long>(kWfStreams, grid / kWfStreams * kWfStreams);
     init_swizzle();
     if (C == 2)

@@ -98,7 +98,7 @@ void transfer_var_(void **mem, real *host_ptr)
 {
     Buffer *b = buf(mem, "transfer_var_");
     if (!b) return;
-    mark_internal(b, nullptr);  // new raw contents
+    mark_internal(b, nullptr, nullptr);  // new raw contents
     b->host_pointer = host_ptr;
     h2d(b, true, nullptr, false);
 }
@@ -107,7 +107,7 @@ void transfer_var_async_(void **mem, real *host_ptr, void **stream, bool *record
 {
     Buffer *b = buf(mem, "transfer_var_async_");
     if (!b) return;
-    mark_internal(b, nullptr);
+    mark_internal(b, nullptr, stream_of(stream));
     b->host_pointer = host_ptr;
     h2d(b, false, stream_of(stream), record_event && *record_event);
 }
@@ -205,7 +205,7 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         report("fct_ale_pre_comm_acc_: scratch or nod_in_elem2D handles too small");
         return;
     }
-    const int limit = num_kernels_limit();
+    const int limit = plan->num_kernels;
     real *tmax = dptr<real>(bmax), *tmin = dptr<real>(bmin);
     if (!run("fct_ale_a1", st, [&] { return f2a::launch_a1(NT, NL, nlev_nod, dptr<real>(blo), dptr<real>(bttf), tmax, tmin, st); })) return;
     if (limit < 2) return finish(1, {bmax, bmin});
@@ -295,7 +295,7 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
         a.hnode_new = dptr<real>(bhn);
         a.del_v = dptr<real>(bdv);
         if (!run("fct_ale_p1v", st, [&] { return f2a::launch_p1v(plan->dev, a, st); })) return;
-        mark_internal(badfh, f2a::p1v_limits_internal(plan->dev, a) ? plan : nullptr);
+        mark_internal(badfh, f2a::p1v_limits_internal(plan->dev, a) ? plan : nullptr, st);
         *alg_state = 7;
         if (!g_resident)
             for (Buffer *b : {bplus, bminus, badfv, bdv})
@@ -396,7 +396,7 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     const int ncols = (int)(std::min(bplus->size, bminus->size) / ((size_t)L * sizeof(real)));
     const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
     if (!plan) return;
-    if (has_internal(badfh)) {
+    if (has_internal(badfh, st)) {
         report("fct_ale_post_comm_acc_: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by "
                "fct_ale_post_comm_h_acc_");
         return;
@@ -501,7 +501,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
-    if (has_internal(badfh)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
+    if (has_internal(badfh, st)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
         report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
         return;
     }
@@ -517,11 +517,11 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                   dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
-    // b3-horizontal folded into the node kernel (default), or its own edge kernel first
-    // (FESOM2_FUSE_B3H=0, or a node with more than kMaxFusedDegree edges)
-    const char *fuse_s = getenv("FESOM2_FUSE_B3H");
-    const int fuse_env = fuse_s ? atoi(fuse_s) : 0;  // measured slower: opt-in
-    const bool fuse = fuse_env != 0 && d.max_degree <= f2a::kMaxFusedDegree;
+    // b3-horizontal as its own edge kernel, then the node kernel.  The tuning build's measured
+    // alternatives: b3h folded into the node kernel (FESOM2_FUSE_B3H), phase 2 as one
+    // persistent launch (FESOM2_P2_WF), chunked phase 2 (FESOM2_P2_CHUNK / FESOM2_P2_MERGE).
+    [[maybe_unused]] const bool fuse = F2A_TUNING && knob("FESOM2_FUSE_B3H", 0) != 0 && d.max_degree <= f2a::kMaxFusedDegree;
+#if F2A_TUNING
     if (fuse) {
         a.n_owned = N;
         a.edge_cnt = plan_edge_counters(plan, ntr);
@@ -529,8 +529,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
             !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
             return;
         if (!run("fct_ale_p2_b3h", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
-    } else if (const char *wf = getenv("FESOM2_P2_WF");
-               wf && atoi(wf) && !comm && ntr == 1 && d.wf_ntiles > 0 && d.wf_G == f2a::fused_group_columns(NL)) {
+    } else if (knob("FESOM2_P2_WF", 0) && !comm && ntr == 1 && d.wf_ntiles > 0 && d.wf_G == f2a::fused_group_columns(NL)) {
         // phase 2 as one persistent launch (b3h and the node kernel interleaved per tile)
         int *state = plan_wf_state(plan);
         if (!state || !ok(hipMemsetAsync(state, 0, sizeof(int) * (16 + (size_t)d.wf_ntiles), st), "hipMemsetAsync(wf)"))
@@ -539,14 +538,14 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         aw.nodes = d.node_rec;
         aw.count = N;
         if (!run("fct_ale_p2_wavefront", st, [&] { return f2a::launch_p2_wavefront(d, aw, state, st); })) return;
-    } else if (const int chunk = getenv("FESOM2_P2_CHUNK") ? atoi(getenv("FESOM2_P2_CHUNK")) : 0;
+    } else if (const int chunk = knob("FESOM2_P2_CHUNK", 0);
                chunk > 0 && !comm && d.p_edge_owner && (int)plan->owner_cum.size() == N + 1) {
         // FESOM2_P2_CHUNK=n: phase 2 in chunks of n nodes of the processing order -- b3h on the edges
         // the chunk owns, then the node kernel on its nodes, so the limited fct_adf_h and plus/minus
         // are re-read from the Infinity Cache (every node's edges belong to its own or an earlier
         // chunk).  Measured break-even at 60k-node chunks (p2 -15 %, b3h +11 % from 2 x 20
         // launches); two-stream pipelining of the chunks was slower.
-        const bool merge = getenv("FESOM2_P2_MERGE") && atoi(getenv("FESOM2_P2_MERGE")) && ntr == 1 &&
+        const bool merge = knob("FESOM2_P2_MERGE", 0) && ntr == 1 &&
                            (NL - 1) % 2 == 0;
         auto edge_range = [&](int c0) {
             const int c1 = std::min(N, c0 + chunk);
@@ -588,7 +587,9 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
             ac.count = c1 - c0;
             if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, ac, st); })) return;
         }
-    } else {
+    } else
+#endif
+    {
         if (!run("fct_ale_b3_horizontal", st, [&] {
                 return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
                                              a.tr, st);
@@ -600,9 +601,12 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
         a.nodes = d.p2_rec + n_first;
         a.count = N - n_first;
+#if F2A_TUNING
         if (fuse) {
             if (!run("fct_ale_p2_b3h_boundary", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
-        } else {
+        } else
+#endif
+        {
             if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
                     return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
                                                  dptr<real>(badfh), a.tr, st);
@@ -657,8 +661,8 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     // the block-internal edges p1v limited already (fct_ale_pre_comm_v_acc_ marked fct_adf_h with
     // its plan): b3h runs on the other edges of that plan's lists only; the mark is cleared once
     // the whole phase has been enqueued
-    const Plan *ip = peek_internal(badfh);
-    if (has_internal(badfh) && !ip) {
+    const Plan *ip = peek_internal(badfh, st);
+    if (has_internal(badfh, st) && !ip) {
         report("fct_ale_post_comm_h_acc_: the mesh plan fct_ale_pre_comm_v_acc_ limited fct_adf_h with was freed");
         return;
     }
@@ -672,16 +676,17 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), nullptr, nullptr, nullptr, nullptr,
                   dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
-    // FESOM2_P2H_FUSE=1: b3-horizontal folded into the c-horizontal node kernel (k_p2hf, arrival
-    // counters decide which endpoint stores the limited flux)
-    const char *fz = getenv("FESOM2_P2H_FUSE");
-    if (!ip && fz && atoi(fz) != 0 && d.max_degree <= f2a::kMaxFusedDegree && (int)plan->owner_cum.size() == N + 1) {
+#if F2A_TUNING
+    // FESOM2_P2H_FUSE=1 (tuning build): b3-horizontal folded into the c-horizontal node kernel
+    // (k_p2hf, arrival counters decide which endpoint stores the limited flux).  The counters are
+    // zeroed at every pass: a pass that stopped between its launches, or two passes on the same mesh
+    // on two streams, would otherwise leave their parity wrong (one mesh, one stream at a time).
+    if (!ip && knob("FESOM2_P2H_FUSE", 0) != 0 && d.max_degree <= f2a::kMaxFusedDegree &&
+        (int)plan->owner_cum.size() == N + 1) {
         a.n_owned = N;
-        const bool fresh = plan->cnt_tracers < ntr;
         a.edge_cnt = plan_edge_counters(plan, ntr);
         if (!a.edge_cnt ||
-            (fresh && !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st),
-                          "hipMemsetAsync(edge counters)")))
+            !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
             return;
         const int owned_edges = plan->owner_cum.back();  // edges with an owned endpoint come first
         if (!run("fct_ale_p2h_b3h", st, [&] { return f2a::launch_p2hf(d, a, st); })) return;
@@ -697,21 +702,27 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
                                              dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
             }))
             return;
-        mark_internal(badfh, nullptr);
+        mark_internal(badfh, nullptr, st);
         *alg_state = 9;
         if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
         return;
     }
-    // FESOM2_B3H_NODE=1 (no exchange): b3h node-centric over the owner order -- exact, measured
-    // 3-17 % slower than the edge-centric two-groups-per-block kernel
-    const char *b3n = getenv("FESOM2_B3H_NODE");
-    const bool b3h_nodes = !ip && !exch && d.p_owner_cum && b3n && atoi(b3n) != 0;
+    // FESOM2_B3H_NODE=1 (tuning build, no exchange): b3h node-centric over the owner order -- exact,
+    // measured 3-17 % slower than the edge-centric two-groups-per-block kernel
+    const bool b3h_nodes = !ip && !exch && d.p_owner_cum && knob("FESOM2_B3H_NODE", 0) != 0;
+#else
+    const bool b3h_nodes = false;
+#endif
     const f2a::MeshPlanDev &de = ip ? ip->dev : d;  // the edge lists b3h runs on
     const int eb = de.n_edge_interior;               // boundary edges (a halo endpoint): [eb, E)
     if (!run("fct_ale_b3_horizontal", st, [&] {
+#if F2A_TUNING
             if (b3h_nodes)
                 return f2a::launch_b3h_nodes(d, NL, plan->owner_cum.back(), E, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);
+#else
+            (void)b3h_nodes;
+#endif
             if (ip) {  // interior edges crossing p1v blocks; without an exchange the boundary ones too
                 const hipError_t e =
                     f2a::launch_b3h_ext(de, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
@@ -735,7 +746,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
         a.count = N - n_first;
         if (!run("fct_ale_p2h_boundary", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
     }
-    mark_internal(badfh, nullptr);
+    mark_internal(badfh, nullptr, st);
     *alg_state = 9;
     if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
 }
@@ -841,7 +852,7 @@ static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_pl
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
-    if (has_internal(badfh)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
+    if (has_internal(badfh, st)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
         report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
         return;
     }
@@ -971,7 +982,7 @@ void fesom2_download_(void **mem, void *host_ptr, int *istat)
 void fesom2_upload_(void **mem, void *host_ptr, int *istat)
 {
     Buffer *b = buf(mem, "fesom2_upload_");
-    if (b) mark_internal(b, nullptr);  // new contents
+    if (b) mark_internal(b, nullptr, nullptr);  // new contents
     *istat = (b && ok(hipMemcpy(b->device_pointer, host_ptr, b->size, hipMemcpyHostToDevice), "H2D")) ? 0 : 1;
 }
 
@@ -1056,8 +1067,17 @@ void fesom2_graph_end_(int *istat, void **s, void **graph)
     *graph = nullptr;
     const hipStream_t st = stream_of(s);
     auto *g = new GraphHandle;
-    if (!capture_close(st, &g->log)) {
-        report("fesom2_graph_end_: the stream has no capture opened by fesom2_graph_begin_ on this thread");
+    bool foreign = false;
+    if (!capture_close(st, &g->log, &foreign)) {
+        if (foreign) {
+            // opened on another thread: end the HIP capture and drop the graph, so that no capture
+            // stays open (an open capture blocks every plan build in the process)
+            report("fesom2_graph_end_: the capture was opened on another thread; it is ended and dropped");
+            hipGraph_t dropped = nullptr;
+            if (hipStreamEndCapture(st, &dropped) == hipSuccess && dropped) (void)hipGraphDestroy(dropped);
+        } else {
+            report("fesom2_graph_end_: the stream has no capture opened by fesom2_graph_begin_");
+        }
         delete g;
         return;
     }
@@ -1085,12 +1105,15 @@ void fesom2_graph_launch_(int *istat, void **graph, void **s)
                    "freed since the capture (capture again)");
             return;
         }
+    if (!marks_replayable(g->log)) return;
     const hipStream_t st = stream_of(s);
     for (const CapturedUse &w : g->log.waits) {
         const Buffer *b = static_cast<const Buffer *>(w.p);
         if (!ok(hipStreamWaitEvent(st, b->event, 0), "hipStreamWaitEvent(graph launch)")) return;
     }
-    if (ok(hipGraphLaunch(g->exec, st), "hipGraphLaunch")) *istat = 0;
+    if (!ok(hipGraphLaunch(g->exec, st), "hipGraphLaunch")) return;
+    marks_apply(g->log);  // the host state the captured calls left behind (fct_adf_h's mark)
+    *istat = 0;
 }
 
 // objects a graph used / buffer events it waits on before each replay (tests and diagnostics)

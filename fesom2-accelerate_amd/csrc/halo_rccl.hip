@@ -130,6 +130,18 @@ void fesom2_comm_free_(void **comm)
     *comm = nullptr;
 }
 
+void fesom2_comm_info_(void **comm, int *rank, int *nranks, int *device, int *istat)
+{
+    *istat = 1;
+    Comm *c = comm_of(comm);
+    if (!c) return;
+    if (!nccl_ok(ncclCommUserRank(c->comm, rank), "ncclCommUserRank") ||
+        !nccl_ok(ncclCommCount(c->comm, nranks), "ncclCommCount") ||
+        !nccl_ok(ncclCommCuDevice(c->comm, device), "ncclCommCuDevice"))
+        return;
+    *istat = 0;
+}
+
 void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_counts,
                        int *send_nodes, int *recv_counts, int *recv_nodes, int *nl, int *istat)
 {

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-from ._paths import lib_path
+from ._paths import engine_name, lib_path
 
 # every exported symbol of include/fesom2-accelerate.h (checked by tests/test_abi.py)
 EXPORTS = (
@@ -25,7 +25,7 @@ EXPORTS = (
     "fesom2_free_pinned_", "fesom2_device_sync_", "fesom2_last_error", "fesom2_event_create_",
     "fesom2_event_record_", "fesom2_event_elapsed_", "fesom2_event_free_",
     "fesom2_kernel_timing_", "fesom2_kernel_timing_reset_", "fesom2_kernel_stats_",
-    "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_halo_plan_",
+    "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_comm_info_", "fesom2_halo_plan_",
     "fesom2_halo_plan_free_", "fct_ale_exchange_acc_", "fct_ale_exchange_post_comm_c_acc_",
     "fct_ale_pre_comm_batched_acc_", "fct_ale_post_comm_c_batched_acc_", "fct_ale_exchange_batched_acc_",
     "fct_ale_exchange_post_comm_c_batched_acc_", "fct_ale_post_comm_iter_acc_",
@@ -42,7 +42,7 @@ def dll():
     """The engine library (loaded once)."""
     global _dll
     if _dll is None:
-        _dll = C.CDLL(lib_path("libfesom2-accelerate.so"))
+        _dll = C.CDLL(lib_path(engine_name()))
         _dll.fesom2_last_error.restype = C.c_char_p
     return _dll
 

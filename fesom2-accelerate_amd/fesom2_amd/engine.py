@@ -393,6 +393,13 @@ class Halo:
                                 arr(rn), ip(nl), C.byref(st))
         check(st, "fesom2_halo_plan_")
 
+    def info(self):
+        """The communicator's own view: {"rank", "nranks", "device"} (fesom2_comm_info_)."""
+        st, r, n, d = C.c_int(0), C.c_int(-1), C.c_int(-1), C.c_int(-1)
+        dll().fesom2_comm_info_(self.comm.ref, C.byref(r), C.byref(n), C.byref(d), C.byref(st))
+        check(st, "fesom2_comm_info_")
+        return {"rank": r.value, "nranks": n.value, "device": d.value}
+
     @staticmethod
     def unique_id():
         uid = (C.c_char * 128)()

@@ -191,6 +191,9 @@ void fesom2_event_free_(void **ev);
 void fesom2_comm_unique_id_(char *id128, int *istat);
 void fesom2_comm_init_(void **comm, char *id128, int *rank, int *nranks, int *istat);
 void fesom2_comm_free_(void **comm);
+/* What the communicator itself reports (ncclCommCount / ncclCommUserRank / ncclCommCuDevice):
+ * lets a host (and bench.py) confirm how many ranks the RCCL exchange actually spans. */
+void fesom2_comm_info_(void **comm, int *rank, int *nranks, int *device, int *istat);
 /* Halo plan: per neighbour rank, the 1-based local node numbers to send (owned) and to receive
  * (halo), concatenated in neighbour order. */
 void fesom2_halo_plan_(void **plan, int *nneigh, int *neigh_ranks, int *send_counts,

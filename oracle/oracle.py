@@ -46,8 +46,6 @@ def lib():
         _lib = C.CDLL(path)
         _lib.oracle_pre_comm.restype = _I
         _lib.oracle_full_pass.restype = _I
-        for name in ("oracle_pre_comm", "oracle_full_pass"):
-            pass
     return _lib
 
 
@@ -193,17 +191,19 @@ def full_pass(m, f, vlimit=1, eps=1e-16, big=1e3, dt=1.0):
     return out
 
 
-def time_full_pass(m, f, budget_s=15.0, max_reps=50):
-    """Time the single-threaded oracle full pass (cpu_baseline leg of bench.py)."""
+def time_full_pass(m, f, budget_s=15.0, max_reps=50, keep=False):
+    """Time the single-threaded oracle full pass (cpu_baseline leg of bench.py).  ``keep``: also
+    return the last pass's outputs (bench.py checks the GPU against them)."""
     t_all = []
+    out = None
     t0 = time.perf_counter()
     while len(t_all) < max_reps:
         t = time.perf_counter()
-        full_pass(m, f)
+        out = full_pass(m, f)
         t_all.append(time.perf_counter() - t)
         if time.perf_counter() - t0 > budget_s:
             break
-    return min(t_all), len(t_all)
+    return (min(t_all), len(t_all), out) if keep else (min(t_all), len(t_all))
 
 
 # --------------------------------------------------------------------------- reference.cpp

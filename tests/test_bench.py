@@ -68,3 +68,72 @@ def test_bench_help_runs_on_cpu():
     out = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), "--help"], capture_output=True,
                          text=True, timeout=120)
     assert out.returncode == 0 and "--graph" in out.stdout
+
+
+# ----------------------------------------------------------------------------- parity check (verify)
+
+class _Args:
+    fct_iter = 1
+    vlimit = 1
+
+
+def test_compare_local_flags_one_changed_cell():
+    """bench.py's check counts every differing cell and reports the largest difference."""
+    import oracle as O
+    m = synth.make_mesh(16, 12, 9, seed=3)
+    f = synth.make_fields(m)
+    want = [O.full_pass(m, f)]
+    got = {k: want[0][k].copy().reshape(1, -1) for k in ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")}
+    bad, max_abs, cells = bench.compare_local(m, got, want)
+    assert not bad and max_abs == 0.0 and cells > 0
+    got["del_h"][0, 5] += 1e-13
+    got["adf_h"][0, -1] = np.nan
+    bad, max_abs, _ = bench.compare_local(m, got, want)
+    assert bad == {"del_h": 1, "adf_h": 1} and max_abs == float("inf")
+
+
+def _verify_worker(rank, world, port, q):
+    """One rank of bench.py's N > 1 check: oracle_local on its strip with the gloo halo."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fesom2_amd import partition
+        g = synth.make_mesh(24, 16, 9, seed=11)
+        m, lists = partition.local_mesh(g, partition.strip_parts(24, 16, world), rank)
+        fields = synth.make_tracer_fields(m, 2)
+        want = bench.oracle_local(m, fields, _Args(), dist, lists)
+        q.put((rank, m.node_gid[: m.N].copy(), m.edge_gid.copy(),
+               [{k: w[k] for k in ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")} for w in want], m.N))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_per_rank_oracle_with_gloo_halo_equals_single_domain():
+    """bench.py's multi-GPU check runs the oracle per rank on its local mesh with the plus/minus halo
+    exchanged over gloo; on every owned cell and local edge that equals the single-domain pass."""
+    import socket
+    import oracle as O
+    mp = pytest.importorskip("torch.multiprocessing")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_verify_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = synth.make_mesh(24, 16, 9, seed=11)
+    L = g.L
+    for k, fk in enumerate(synth.make_tracer_fields(g, 2)):
+        want = O.full_pass(g, fk)
+        for rank, gid, egid, outs, n in res:
+            o = outs[k]
+            for name, w in (("plus", L), ("minus", L), ("del_v", L), ("del_h", L), ("adf_v", g.nl)):
+                assert np.array_equal(o[name].reshape(-1, w)[:n], want[name].reshape(-1, w)[gid]), (rank, k, name)
+            assert np.array_equal(o["adf_h"].reshape(-1, L), want["adf_h"].reshape(-1, L)[egid]), (rank, k)

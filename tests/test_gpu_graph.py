@@ -105,13 +105,12 @@ def test_replay_waits_for_async_uploads():
         dm.free()
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_replay_with_halo_exchange_two_tracers(comm, fuse, monkeypatch):
+@pytest.mark.parametrize("internal", ["0", "1"])
+def test_replay_with_halo_exchange_two_tracers(comm, internal, monkeypatch):
     """Two tracers of a partitioned mesh in ONE graph, each pre_comm_v -> post_comm_h(comm, plan) with
     the same halo plan (its stream and events reused twice in the capture).  Halo plus/minus are
     uploaded deranged before each replay; owned results must equal the single-domain oracle."""
-    monkeypatch.setenv("FESOM2_P2H_FUSE", fuse)  # b3h folded into c-horizontal, or partly into p1v
-    monkeypatch.setenv("FESOM2_P1V_B3H", "0" if fuse == "1" else "1")
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)  # block-internal edges limited in p1v, or all in b3h
     nx, ny, nl, nranks, ntr = 64, 48, 21, 2, 2
     gm = synth.make_mesh(nx, ny, nl)
     gfields = synth.make_tracer_fields(gm, ntr)
@@ -280,3 +279,108 @@ def test_capture_state_is_per_stream():
         e.free()
         dm.free()
         other.free()
+
+
+def _split_outputs(e):
+    return {k: e.download(k) for k in OUT}
+
+
+def _reupload(e):
+    for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+        e.upload(k)
+
+
+@pytest.mark.parametrize("captured", ["pre_comm_v", "post_comm_h"])
+def test_half_pass_graph_with_eager_other_half(captured, monkeypatch):
+    """fct_adf_h's internal-edge mark (host state) follows the replays: a graph holding only
+    pre_comm_v leaves fct_adf_h marked after each launch, so an eager post_comm_h skips the edges p1v
+    limited; a graph holding only post_comm_h checks before each launch that an eager pre_comm_v
+    marked it (and refuses to run otherwise).  Three steps each, exact every time."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", "1")
+    m = synth.config_mesh("8k x 20")
+    f = synth.make_fields(m)
+    want = O.full_pass(m, f)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    g = None
+    try:
+        assert dm.info()["internal_edges"] > 0
+        assert e.split_pass() == 9, abi.last_error()  # plans
+        _reupload(e)
+        e.sync()
+        if captured == "pre_comm_v":
+            with abi.Graph.capture(e.stream) as g:
+                assert e.pre_comm_v() == 7, abi.last_error()
+            for _ in range(3):
+                _reupload(e)
+                g.launch(e.stream)
+                assert e.post_comm_h() == 9, abi.last_error()
+                e.sync()
+                check_pass(m, _split_outputs(e), want)
+        else:
+            assert e.pre_comm_v() == 7, abi.last_error()  # marks fct_adf_h
+            with abi.Graph.capture(e.stream) as g:
+                assert e.post_comm_h() == 9, abi.last_error()
+            e.sync()
+            for step in range(3):
+                if step:
+                    _reupload(e)
+                    assert e.pre_comm_v() == 7, abi.last_error()
+                g.launch(e.stream)
+                e.sync()
+                check_pass(m, _split_outputs(e), want)
+            # the mark was consumed by the last replay: another replay without pre_comm_v is refused
+            with pytest.raises(abi.HipError, match="fct_adf_h"):
+                g.launch(e.stream)
+    finally:
+        if g is not None:
+            g.free()
+        e.free()
+        dm.free()
+
+
+def test_graph_end_on_another_thread_does_not_block_plan_builds():
+    """fesom2_graph_end_ from a thread other than the one that began the capture fails, but ends
+    the HIP capture and unregisters it: later plan builds (which refuse to run while any capture is
+    open) still work, and the opening thread can capture again."""
+    import threading
+    m = synth.config_mesh("tiny")
+    f = synth.make_fields(m)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.split_pass() == 9
+        e.sync()
+        st = C.c_int(0)
+        dll().fesom2_graph_begin_(C.byref(st), e.stream.ref)
+        assert st.value == 0, abi.last_error()
+        result = {}
+
+        def end_elsewhere():
+            g = abi.Graph()
+            s2 = C.c_int(0)
+            dll().fesom2_graph_end_(C.byref(s2), e.stream.ref, g.ref)
+            result["st"], result["graph"] = s2.value, bool(g)
+
+        t = threading.Thread(target=end_elsewhere)
+        t.start()
+        t.join()
+        assert result == {"st": 1, "graph": False}
+        # a fresh mesh needs a plan build: not blocked by an orphaned capture
+        m2 = synth.config_mesh("tiny", full_depth=True)
+        dm2 = engine.DeviceMesh(m2)
+        e2 = engine.FctAle(dm2, synth.make_fields(m2))
+        try:
+            assert e2.split_pass() == 9, abi.last_error()
+            e2.sync()
+        finally:
+            e2.free()
+            dm2.free()
+        # and this thread can open and close a capture again
+        with abi.Graph.capture(e.stream) as g:
+            assert e.pre_comm_v() == 7
+            assert e.post_comm_h() == 9
+        g.free()
+    finally:
+        e.free()
+        dm.free()

@@ -83,30 +83,6 @@ def test_full_pass_matches_oracle(name, full, perm, fused, path):
     check_pass(m, got, want)
 
 
-KNOBS = [{"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "0"}, {"FESOM2_B3H_U": "4", "FESOM2_B3H_NT": "0"},
-         {"FESOM2_B3H_U": "1", "FESOM2_B3H_NT": "1"}, {"FESOM2_B3H_CPT": "4"}, {"FESOM2_NT": "3"},
-         {"FESOM2_P1_BATCH": "44", "FESOM2_P2_BATCH": "8"}, {"FESOM2_PATCH": "0"}, {"FESOM2_PATCH": "7"}, {"FESOM2_FUSE_B3H": "1"},
-         {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "1"}, {"FESOM2_FUSE_B3H": "1", "FESOM2_P2F_BATCH": "4"},
-         {"FESOM2_P1_STAGE": "1", "FESOM2_P1_EDGE": "0"},
-         {"FESOM2_P1_STAGE": "1", "FESOM2_P1_EDGE": "0", "FESOM2_P1S_EB": "4"}, {"FESOM2_P1_EDGE": "0"},
-         {"FESOM2_P1E_EB": "1"}, {"FESOM2_P1E_EB": "4"}, {"FESOM2_NT": "0"}, {"FESOM2_P2_CPT": "1"},
-         {"FESOM2_P2_CPT": "1", "FESOM2_NT": "0"}, {"FESOM2_P2_CHUNK": "1000"},
-         {"FESOM2_P2_CHUNK": "37", "FESOM2_B3H_NT": "0"}, {"FESOM2_P2_WF": "1"},
-         {"FESOM2_P2_CHUNK": "1000", "FESOM2_P2_MERGE": "1"}, {"FESOM2_P2_CHUNK": "333", "FESOM2_P2_MERGE": "1"}]
-
-
-@pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
-@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
-def test_kernel_variants_match_oracle(knobs, name, monkeypatch):
-    """Every tuning variant the launchers can select (env knobs read at launch) is exact too."""
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
-    m, f = mesh(name)
-    st, got = run_pass(m, f)
-    assert st == 9
-    check_pass(m, got, O.full_pass(m, f))
-
-
 @pytest.mark.parametrize("vlimit", [2, 3])
 @pytest.mark.parametrize("path", ["fused", "stepwise"])
 def test_vlimit_variants(vlimit, path):
@@ -470,32 +446,17 @@ def test_degenerate_level_counts(kind, mode, monkeypatch):
     check_pass(m, got, O.full_pass(m, f, vlimit=vl))
 
 
-SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1V_EARLY": "8"},
-               {"FESOM2_ODD_PAIR": "0"}, {"FESOM2_NL_PAIR": "0"}, {"FESOM2_NL_PAIR": "0", "FESOM2_NT": "0"},
-               {"FESOM2_PATCH_ORDER": "1"}, {"FESOM2_PATCH_ORDER": "1", "FESOM2_PATCH": "100"},
-               {"FESOM2_PATCH_ORDER": "0", "FESOM2_PATCH": "64"}, {"FESOM2_B3H_NODE": "1"},
-               {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "1"}, {"FESOM2_B3H_NODE": "1", "FESOM2_B3HN_EB": "3"},
-               {"FESOM2_B3H_NODE": "1", "FESOM2_ODD_PAIR": "0"}, {"FESOM2_B3H_PACK": "0"},
-               {"FESOM2_B3H_PACK": "1", "FESOM2_B3H_NT": "0"},
-               {"FESOM2_B3HP_H": "1"}, {"FESOM2_B3HP_H": "4"}, {"FESOM2_B3HP_CAP": "100"},
-               {"FESOM2_P2H_FUSE": "1"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "1"},
-               {"FESOM2_P2H_FUSE": "1", "FESOM2_P2HF_KB": "4"}, {"FESOM2_P2H_FUSE": "1", "FESOM2_NT": "0"},
-               {"FESOM2_P2H_FUSE": "1", "FESOM2_ODD_PAIR": "0"}, {"FESOM2_P1V_B3H": "0"},
-               {"FESOM2_P1V_B3H": "1", "FESOM2_SUBPATCH": "8"}, {"FESOM2_P1V_B3H": "1", "FESOM2_NL_PAIR": "0"},
-               {"FESOM2_P1V_B3H": "1", "FESOM2_CPT": "1"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3H_PACK": "0"},
-               {"FESOM2_NT": "2"}, {"FESOM2_NT": "2", "FESOM2_P1V_B3H": "1"}, {"FESOM2_NT": "6", "FESOM2_P1V_B3H": "0"},
-               {"FESOM2_BLOB": "1"}, {"FESOM2_BLOB": "1", "FESOM2_PATCH_ORDER": "1"}, {"FESOM2_BLOB": "0"},
-               {"FESOM2_P1V_B3H": "1", "FESOM2_P1V_INT_DMA": "0"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3HP_REG": "0"}]
+# plan options of the product library (read once when a mesh plan is built)
+PLAN_OPTIONS = [{"FESOM2_P1V_B3H": "0"}, {"FESOM2_P1V_B3H": "1"}, {"FESOM2_PATCH": "64"}, {"FESOM2_PATCH": "0"},
+                {"FESOM2_PATCH": "100", "FESOM2_P1V_B3H": "1"}, {"FESOM2_PATCH": "4096", "FESOM2_P1V_B3H": "1"}]
 
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
 @pytest.mark.parametrize("full", [False, True])
-@pytest.mark.parametrize("mode", ["p2h_fuse", "p1v_internal"])
-def test_fused_b3h_level_counts_and_repeats(nl, full, mode, monkeypatch):
-    """FESOM2_P2H_FUSE=1 (b3h folded into c-horizontal, arrival counters that are never reset) and
-    FESOM2_P1V_B3H=1 (block-internal edges limited in p1v): three passes on the same plan, inputs
+def test_internal_edges_level_counts_and_repeats(nl, full, monkeypatch):
+    """FESOM2_P1V_B3H=1 (block-internal edges limited in p1v): three passes on the same plan, inputs
     re-uploaded before each, every one exact."""
-    monkeypatch.setenv("FESOM2_P2H_FUSE" if mode == "p2h_fuse" else "FESOM2_P1V_B3H", "1")
+    monkeypatch.setenv("FESOM2_P1V_B3H", "1")
     m = synth.make_mesh(40, 14, nl, full_depth=full)
     f = synth.make_fields(m)
     want = O.full_pass(m, f)
@@ -547,11 +508,11 @@ def test_block_internal_edges(name, monkeypatch):
         dm.free()
 
 
-@pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("knobs", PLAN_OPTIONS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
 @pytest.mark.parametrize("name,perm", [("8k x 20", False), ("8k x 20", True), ("127k x 47", False)])
-def test_split_variants_match_oracle(knobs, name, perm, monkeypatch):
-    """The direction-split kernels' switches (p1v load placement, LDS-DMA tail, odd-L pairs,
-    16-byte stride-nl loads, processing orders) are all exact."""
+def test_split_plan_options_match_oracle(knobs, name, perm, monkeypatch):
+    """The plan options (block-internal edges in p1v or not, patch sizes incl. index order) are all
+    exact on the direction-split pass."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     m, f = mesh(name, False, perm)

@@ -5,6 +5,8 @@
 # A configuration may carry bench arguments after " | " ("FESOM2_X=1 | --path split").
 # BENCH_ARGS (eval'ed: may quote), STEPS, ROUNDS.
 set -o pipefail
+# the knobs exist in the tuning build only (make -C fesom2-accelerate_amd tuning)
+export FESOM2_LIB_NAME=${FESOM2_LIB_NAME:-libfesom2-accelerate-tuning.so}
 out=gpurun_out/sweep.txt
 : > $out
 for r in $(seq 1 ${ROUNDS:-1}); do
