@@ -99,6 +99,8 @@ def kernel_bytes(s, ntr=1, split=False):
     # c-horizontal with b3h folded in: raw adf_h read, limited adf_h written once, plus/minus of both
     # endpoints (owned + halo columns), del_h rw; area shared
     p2hf = ntr * 8 * (2 * cn + 2 * ce + 2 * (cn + ch)) + 8 * cn + 4 * N + ints_edges + 4 * E
+    # reference entry sequence in the fast mode: phase 1 + b3v (+ the internal edges) in one kernel
+    p1b3v = p1 + ntr * 8 * (cn + ice) + 16 * nie
     # reference entry sequence on the fused kernels: b3v alone (plus/minus, adf_v rw) and the c-step
     # node kernel (cv + ch: del_v, del_h rw; ttf, LO, adf_v, adf_h; area, hnode, hnode_new shared)
     b3v = ntr * 8 * (2 * cn + 2 * cn1) + 4 * N
@@ -106,7 +108,7 @@ def kernel_bytes(s, ntr=1, split=False):
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
     return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
             "fct_ale_p1v": p1v, "fct_ale_p2h": p2h, "fct_ale_p2h_b3h": p2hf,
-            "fct_ale_b3_vertical": b3v, "fct_ale_c": c_step,
+            "fct_ale_b3_vertical": b3v, "fct_ale_c": c_step, "fct_ale_p1_b3v": p1b3v,
             "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 
@@ -324,7 +326,8 @@ def main():
     ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference"],
                     help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
                          "stepwise: one kernel per reference step; reference: the reference's entry sequence "
-                         "pre_comm -> inter_comm -> post_comm -> c with the fused phase 1")
+                         "pre_comm -> inter_comm -> post_comm -> c in its fast mode (fesom2_set_path_(2): b3v "
+                         "and the block-internal edges inside pre_comm)")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
     ap.add_argument("--graph", action="store_true",
@@ -415,7 +418,7 @@ def main():
         fields = [pf]
         f = pf
     abi.set_resident(not args.transfers)
-    abi.set_path("stepwise" if args.path == "stepwise" else "fused")
+    abi.set_path({"stepwise": "stepwise", "reference": "reference"}.get(args.path, "fused"))
     dm = engine.DeviceMesh(m)
     dm.prepare()
     mi = dm.info()
@@ -557,7 +560,7 @@ def main():
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
     s = mesh_stats(m)
     s.update(mesh_info)
-    kb = kernel_bytes(s, args.tracers, split=args.path == "split")
+    kb = kernel_bytes(s, args.tracers, split=args.path in ("split", "reference"))
     per_kernel = {}
     for name, (cnt, tot) in stats.items():
         avg = tot / max(cnt, 1)

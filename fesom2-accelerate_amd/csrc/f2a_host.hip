@@ -52,12 +52,14 @@ int kernel_path()
 {
     if (g_path < 0) {
         const char *p = getenv("FESOM2_PATH");
-        g_path = (p && (!strcmp(p, "stepwise") || !strcmp(p, "1"))) ? 1 : 0;
+        g_path = (p && (!strcmp(p, "stepwise") || !strcmp(p, "1"))) ? 1
+                 : (p && (!strcmp(p, "reference") || !strcmp(p, "2"))) ? 2
+                                                                          : 0;
     }
     return g_path;
 }
 
-void set_kernel_path(int p) { g_path = p == 1 ? 1 : 0; }
+void set_kernel_path(int p) { g_path = (p == 1 || p == 2) ? p : 0; }
 
 
 Buffer *buf(void **h, const char *name)

@@ -29,7 +29,8 @@ unsigned long error_count();  // number of report() calls so far (all threads)
 
 // ---- global modes
 extern int g_resident;  // fesom2_set_resident_
-int kernel_path();      // 0 fused, 1 stepwise (fesom2_set_path_; FESOM2_PATH, read once, sets the default)
+int kernel_path();      // 0 fused, 1 stepwise, 2 reference-sequence fast mode (fesom2_set_path_;
+                        // FESOM2_PATH, read once, sets the default)
 void set_kernel_path(int p);
 
 // ---- handles
@@ -182,8 +183,10 @@ struct MeshHandles {
 const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
                      bool with_ring);
 void drop_plans_of(const Buffer *b);
-// fct_adf_h's internal-edge marker (Buffer::int_plan): set after a p1v launch that limited the
-// block-internal edges of `plan` (nullptr clears).  `s` is the stream of the call (nullptr for the
+// Phase marks (Buffer::int_plan) -- part of phase 2 already done by a phase-1 launch: on fct_adf_h
+// the block-internal edges of `plan` limited by p1v (fct_ale_pre_comm_v_acc_, or fct_ale_pre_comm_acc_
+// in the fast mode); on fct_adf_v b3-vertical done by fct_ale_pre_comm_acc_ in the fast mode
+// (fct_ale_inter_comm_acc_ then has nothing left to compute).  nullptr clears.  `s` is the stream of the call (nullptr for the
 // synchronous uploads): on a captured stream the access is recorded in the capture's log.
 void mark_internal(Buffer *adf_h, const Plan *plan, hipStream_t s);
 bool has_internal(Buffer *adf_h, hipStream_t s);

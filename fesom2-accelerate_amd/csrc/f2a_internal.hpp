@@ -44,8 +44,9 @@ struct Buffer {
     hipEvent_t event = nullptr;
     bool has_event = false;
     uint64_t serial = 0;  // live-object serial (track_object): graph replays check it is unchanged
-    // fct_adf_h only: the mesh plan whose block-internal edges fct_ale_pre_comm_v_acc_ limited in
-    // p1v (fct_ale_post_comm_h_acc_ then limits the others; cleared by it and by every upload)
+    // phase mark (f2a_host.hpp): on fct_adf_h the mesh plan whose block-internal edges a p1v launch
+    // limited (the phase-2 entry then limits the others), on fct_adf_v the plan whose phase-1 launch
+    // did b3-vertical; cleared by the entry that finishes the phase and by every upload
     const void *int_plan = nullptr;
     uint64_t int_serial = 0;
 };
@@ -191,6 +192,9 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 // phase 1 + the vertical half of phase 2 (b3v, cv need only the node's own column: no halo), then
 // phase 2's horizontal half alone (launch_p2h: c-horizontal; b3h stays its own kernel)
 hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
+// phase 1 + b3v (+ the block-internal edges' b3h), no cv: fct_ale_pre_comm_acc_ in the reference
+// sequence's fast mode (no area/hnode/hnode_new/del_v needed)
+hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // columns per p1v block for nl levels at vlimit 1 (the shape launch_p1v uses; the plan's int_G)
 int p1v_group_columns(int nl);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)

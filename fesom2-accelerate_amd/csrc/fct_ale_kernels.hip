@@ -315,7 +315,9 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // column, so they need no halo exchange): plus/minus go through LDS to the neighbouring level slots,
 // fct_adf_v is limited from the raw values the thread already holds and written after the barriers
 // (every raw fct_adf_v read of the block happened before the first one), and del_ttf_advvert is
-// updated -- the arithmetic of k_p2, so results are identical.
+// updated -- the arithmetic of k_p2, so results are identical.  OPT & 64: b3v only, no cv (the
+// reference entry sequence's fct_ale_pre_comm_acc_ in the fast mode: it has no del_ttf_advvert,
+// hnode, hnode_new or area; fct_ale_c_acc_ does cv).
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
 __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float invS)
 {
@@ -331,7 +333,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
         a.minus += tr * a.tr.node;
         a.adf_v += tr * a.tr.lev;
         a.adf_h += tr * a.tr.edge;
-        if (VERT) a.del_v += tr * a.tr.node;
+        if (VERT && !(OPT & 64)) a.del_v += tr * a.tr.node;
     }
     const int ncol = min(G, a.n_owned - first);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
@@ -632,7 +634,9 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
             lim[c] = lim_here ? b3v_factor(z, v[c], pp[c], mm[c], pp[c + 1], mm[c + 1]) * v[c] : v[c];
         }
         real dv[C];
-        if ((OPT & 2) && nw > 0) {
+        if constexpr (OPT & 64) {
+            (void)dv;
+        } else if ((OPT & 2) && nw > 0) {
 #pragma unroll
             for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
         } else if (nw > 0) {
@@ -671,7 +675,8 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
                 t.y = lim[1];
                 *reinterpret_cast<f2a_d2u *>(const_cast<real *>(a.adf_v) + ab) = t;
             }
-        if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
+        if constexpr (!(OPT & 64))
+            if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
     }
 }
 
@@ -1488,6 +1493,50 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
 #endif
+}
+
+// phase 1 + b3-vertical (+ the block-internal edges' b3-horizontal) without c-vertical: the
+// reference sequence's fct_ale_pre_comm_acc_ in the fast mode (fesom2_set_path_(2))
+hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
+{
+    const bool in = p1v_limits_internal(mp, a);
+    const int L = a.nl - 1;
+    if (odd_pairs(L) && a.vlimit == 1) {
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = p1_lds_bytes(G, L, 1, in);
+        const float inv = 1.0f / (float)S;
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+    }
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+    const float invS = 1.0f / (float)S;
+    const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
+    if (C == 2) {
+        switch (a.vlimit) {
+        case 2:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        case 3:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        default:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        }
+    }
+    switch (a.vlimit) {
+    case 2:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true, 16 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true, 64>), groups, G, S, lds, s, mp, a, G, invS);
+    case 3:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 16 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<3, 1, 2, 2, false, true, 64>), groups, G, S, lds, s, mp, a, G, invS);
+    default:
+        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 16 | 64>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_p1<1, 1, 2, 2, false, true, 64>), groups, G, S, lds, s, mp, a, G, invS);
+    }
 }
 
 hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)

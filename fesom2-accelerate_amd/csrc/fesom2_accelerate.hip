@@ -193,7 +193,20 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         f2a::P1Args a{N, NL, *vlimit, nlev_nod, dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
                       dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
                       *dt, *flux_eps, *bignumber};
-        if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) return;
+        if (kernel_path() == 2) {
+            // fast mode: b3-vertical (and the block-internal edges' b3-horizontal) while the block's
+            // plus/minus are in LDS; inter_comm / post_comm find the marks and do the rest
+            if (has_internal(badfv, st) || has_internal(badfh, st)) {
+                report("fct_ale_pre_comm_acc_: fct_adf_v/fct_adf_h already hold a limited phase 2 part (upload "
+                       "the raw fluxes first)");
+                return;
+            }
+            if (!run("fct_ale_p1_b3v", st, [&] { return f2a::launch_p1_b3v(plan->dev, a, st); })) return;
+            mark_internal(badfv, plan, st);
+            mark_internal(badfh, f2a::p1v_limits_internal(plan->dev, a) ? plan : nullptr, st);
+        } else if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) {
+            return;
+        }
         finish(6, {bplus, bminus});
         return;
     }
@@ -362,6 +375,14 @@ void fct_ale_inter_comm_acc_(int *alg_state, void **s, void **fct_plus, void **f
     Buffer *badfv = need(fct_adf_v, col_bytes(N, NL), "fct_adf_v");
     Buffer *bnl = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
     if (!bplus || !bminus || !badfv || !bnl) return;
+    if (has_internal(badfv, st)) {
+        // fast mode: fct_ale_pre_comm_acc_ limited fct_adf_v already (reference :342-356 computed
+        // b3v here); what is left is the reference's transfer back
+        mark_internal(badfv, nullptr, st);
+        *alg_state = 7;
+        if (!g_resident && !d2h_async(badfv, st)) *alg_state = 0;
+        return;
+    }
     const bool stepwise = kernel_path() == 1;
     if (!run("fct_ale_b3_vertical", st, [&] {
             return stepwise ? f2a::launch_b3v(N, NL, dptr<int>(bnl), dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfv), st)
@@ -396,15 +417,30 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     const int ncols = (int)(std::min(bplus->size, bminus->size) / ((size_t)L * sizeof(real)));
     const Plan *plan = get_plan(mh, 0, ncols, E, NL, false);
     if (!plan) return;
-    if (has_internal(badfh, st)) {
-        report("fct_ale_post_comm_acc_: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by "
-               "fct_ale_post_comm_h_acc_");
+    // fast mode: the block-internal edges were limited by fct_ale_pre_comm_acc_ (marked with its
+    // plan, whose lists say which); b3h runs on the others
+    const Plan *ip = peek_internal(badfh, st);
+    if (has_internal(badfh, st) && !ip) {
+        report("fct_ale_post_comm_acc_: the mesh plan that limited part of fct_adf_h was freed");
+        return;
+    }
+    if (ip && (ip->dev.n_edges != E || ip->dev.n_total > ncols)) {
+        report("fct_ale_post_comm_acc_: fct_adf_h was partly limited on another mesh");
         return;
     }
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
     // fused path: the production edge kernel over the plan's edge list (edge index order here)
     const bool stepwise = kernel_path() == 1;
     if (!run("fct_ale_b3_horizontal", st, [&] {
+            if (ip) {  // interior edges crossing p1v blocks, then the boundary ones
+                const f2a::MeshPlanDev &de = ip->dev;
+                const hipError_t e = f2a::launch_b3h_ext(de, NL, dptr<real>(bplus), dptr<real>(bminus),
+                                                         dptr<real>(badfh), f2a::Tracers{}, st);
+                const int eb = de.n_edge_interior;
+                if (e != hipSuccess || eb >= E) return e;
+                return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
+                                             dptr<real>(badfh), f2a::Tracers{}, st);
+            }
             if (!stepwise && plan->dev.p_edge_info)
                 return f2a::launch_b3h_fused(plan->dev, NL, 0, E, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
                                              f2a::Tracers{}, st);
@@ -412,6 +448,7 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
                                    dptr<real>(bminus), dptr<real>(badfh), st);
         }))
         return;
+    mark_internal(badfh, nullptr, st);
     *alg_state = 8;
     if (!g_resident && !d2h_async(badfh, st)) *alg_state = 0;
 }
@@ -501,8 +538,9 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
-    if (has_internal(badfh, st)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
-        report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
+    if (has_internal(badfh, st) || has_internal(badfv, st)) {  // part of phase 2 done already
+        report("%s: fct_adf_h/fct_adf_v come from fct_ale_pre_comm_v_acc_ (finished by fct_ale_post_comm_h_acc_) or "
+               "from the fast mode's fct_ale_pre_comm_acc_ (finished by inter_comm and post_comm)", who);
         return;
     }
     if (!g_resident && !comm && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;
@@ -852,8 +890,9 @@ static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_pl
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
-    if (has_internal(badfh, st)) {  // fct_ale_pre_comm_v_acc_ already limited part of fct_adf_h
-        report("%s: fct_adf_h comes from fct_ale_pre_comm_v_acc_, which is finished by fct_ale_post_comm_h_acc_", who);
+    if (has_internal(badfh, st) || has_internal(badfv, st)) {  // part of phase 2 done already
+        report("%s: fct_adf_h/fct_adf_v come from fct_ale_pre_comm_v_acc_ or the fast mode's fct_ale_pre_comm_acc_; "
+               "iter_yn needs the raw fluxes (fesom2_set_path_(0))", who);
         return;
     }
     if (!g_resident) {

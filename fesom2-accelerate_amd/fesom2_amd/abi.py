@@ -206,7 +206,10 @@ def set_resident(on):
 
 
 def set_path(path):
-    dll().fesom2_set_path_(ip(1 if path in ("stepwise", 1) else 0))
+    """fesom2_set_path_: "fused" (0), "stepwise" (1), or "reference" (2: the reference entry
+    sequence's fast mode, b3v inside fct_ale_pre_comm_acc_)."""
+    code = {"fused": 0, "stepwise": 1, "reference": 2}.get(path, path)
+    dll().fesom2_set_path_(ip(code))
 
 
 def device_sync():

@@ -129,7 +129,11 @@ void fesom2_reserve_var_i8_(void **ret, long long *size, bool *create_event, int
  * fct_adf_h, c downloads del_ttf_*.  1 = device resident: no implicit host transfers. */
 void fesom2_set_resident_(int *resident);
 /* Kernel path.  0 (default) = fused node-centric kernels; 1 = one kernel per reference step
- * (materialises fct_ttf_max/min and UV_rhs, honours FESOM2_NUM_KERNELS for bisection). */
+ * (materialises fct_ttf_max/min and UV_rhs, honours FESOM2_NUM_KERNELS for bisection); 2 = the
+ * reference entry sequence's fast mode: fct_ale_pre_comm_acc_ also does b3-vertical (the node's own
+ * plus/minus are final after b2) and the block-internal edges' b3-horizontal, fct_ale_inter_comm_acc_
+ * then only moves fct_adf_v, fct_ale_post_comm_acc_ limits the remaining edges.  Same results;
+ * phase-2 entries other than inter_comm/post_comm refuse fct_adf_v/fct_adf_h touched this way. */
 void fesom2_set_path_(int *path);
 /* Build the derived mesh structures (edge/ring CSR) ahead of the first pass (otherwise built
  * lazily, synchronously, on first use). */

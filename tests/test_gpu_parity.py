@@ -74,7 +74,7 @@ CASES = [("tiny", False, False), ("8k x 20", False, False), ("8k x 20", True, Fa
 
 
 @pytest.mark.parametrize("name,full,perm", CASES)
-@pytest.mark.parametrize("fused,path", [(True, "fused"), (False, "fused"), (False, "stepwise")])
+@pytest.mark.parametrize("fused,path", [(True, "fused"), (False, "fused"), (False, "stepwise"), (False, "reference")])
 def test_full_pass_matches_oracle(name, full, perm, fused, path):
     m, f = mesh(name, full, perm)
     want = O.full_pass(m, f)
@@ -599,3 +599,57 @@ def test_graph_replay_matches_oracle():
     finally:
         e2.free()
         dm2.free()
+
+
+@pytest.mark.parametrize("name,full", [("8k x 20", False), ("8k x 20", True), ("127k x 47", False), ("tiny", True)])
+@pytest.mark.parametrize("resident", [True, False])
+@pytest.mark.parametrize("internal", ["0", "1"])
+@pytest.mark.parametrize("vlimit", [1, 2])
+def test_reference_sequence_fast_mode(name, full, resident, internal, vlimit, monkeypatch):
+    """fesom2_set_path_(2): the unmodified reference sequence pre_comm -> inter_comm -> post_comm -> c
+    with b3v (and the block-internal edges) done inside pre_comm; every output exact, with the
+    reference's transfer semantics too (inter_comm still hands the host the limited fct_adf_v)."""
+    monkeypatch.setenv("FESOM2_P1V_B3H", internal)
+    m, f = mesh(name, full)
+    st, p1 = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
+    want = O.post_comm(m, f, p1["plus"], p1["minus"])
+    abi.set_resident(resident)
+    abi.set_path("reference")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f, vlimit=vlimit)
+    pristine = {k: e.host[k].copy() for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")}
+    try:
+        for _ in range(2):  # twice on the same buffers: the marks are consumed every pass
+            for k, v in pristine.items():
+                e.host[k][:] = v  # (the reference transfers wrote the outputs into the host arrays)
+                e.upload(k)
+            assert e.pre_comm() == 6, abi.last_error()
+            assert e.inter_comm() == 7, abi.last_error()
+            assert e.post_comm() == 8, abi.last_error()
+            assert e.c_step() == 9, abi.last_error()
+            e.sync()
+            for k in ("adf_v", "adf_h", "del_v", "del_h"):
+                got = e.host[k] if not resident else e.download(k)
+                assert np.array_equal(got, want[k]), k
+    finally:
+        abi.set_resident(True)
+        abi.set_path("fused")
+        e.free()
+        dm.free()
+
+
+def test_fast_mode_marks_refuse_other_phase_2():
+    """After a fast-mode fct_ale_pre_comm_acc_ the fused phase 2 would limit fct_adf_v twice: it
+    refuses; a second pre_comm without fresh fluxes refuses too."""
+    m, f = mesh("8k x 20")
+    abi.set_path("reference")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        assert e.pre_comm() == 6, abi.last_error()
+        assert e.post_comm_c() != 9 and "fct_adf_v" in abi.last_error()
+        assert e.pre_comm() != 6 and "upload" in abi.last_error()
+    finally:
+        abi.set_path("fused")
+        e.free()
+        dm.free()
