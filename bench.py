@@ -427,6 +427,8 @@ def main():
         raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
     e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
         engine.FctAleBatch(dm, fields, vlimit=args.vlimit)
+    if args.path == "reference" and not args.transfers:
+        e.bind_c_vertical()  # the fast mode's c-vertical inside pre_comm (fesom2_bind_c_vertical_)
     stream = e.stream
 
     halo = None

@@ -49,6 +49,14 @@ struct Buffer {
     // did b3-vertical; cleared by the entry that finishes the phase and by every upload
     const void *int_plan = nullptr;
     uint64_t int_serial = 0;
+    // fct_adf_v only: the c-step's vertical fields bound by fesom2_bind_c_vertical_ (owned)
+    struct CvBinding *cv = nullptr;
+};
+
+// fesom2_bind_c_vertical_: del_ttf_advvert, hnode, hnode_new, area with their live serials
+struct CvBinding {
+    Buffer *b[4];
+    uint64_t serial[4];
 };
 
 // One incident edge of a node in the node->edge CSR (ascending edge order per node, which is the

@@ -319,23 +319,21 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // reference entry sequence's fct_ale_pre_comm_acc_ in the fast mode: it has no del_ttf_advvert,
 // hnode, hnode_new or area; fct_ale_c_acc_ does cv).
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
-__device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float invS)
+__device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
-    const int L = a.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
+    // OPT & 128 (VERT): the block runs its G columns for every tracer of the batch in turn -- the
+    // records, the internal-edge entries and the slot geometry are set up once, and the shared mesh
+    // fields (area_inv, area, hnode, hnode_new) of the block's columns come back from L2 for the
+    // later tracers.  Otherwise tiles are (column group, tracer).
+    constexpr bool TLOOP = (OPT & 128) != 0;
+    static_assert(!TLOOP || VERT, "the tracer loop keeps every thread in every barrier: VERT forms only");
+    const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
-    int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 1) * G;
-    if (tr) {
-        a.ttf += tr * a.tr.node;
-        a.LO += tr * a.tr.node;
-        a.plus += tr * a.tr.node;
-        a.minus += tr * a.tr.node;
-        a.adf_v += tr * a.tr.lev;
-        a.adf_h += tr * a.tr.edge;
-        if (VERT && !(OPT & 64)) a.del_v += tr * a.tr.node;
-    }
-    const int ncol = min(G, a.n_owned - first);
+    int tr0 = 0;
+    const int first = (TLOOP ? block_tile() : group_tracer(a0.tr.n, tr0, c_tracer_major & 1)) * G;
+    const int ntl = TLOOP ? a0.tr.n : 1;
+    const int ncol = min(G, a0.n_owned - first);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
     // after b2, from the plus/minus in LDS.  Wave 0 stages their entries and slot offsets (one
     // per lane, exclusive scan of ceil(lev/C)) while the records load.
@@ -384,8 +382,27 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
     const int z0 = C * u;
     const bool last1 = ODD && z0 + 1 == L;
     const bool col = j < ncol;
+#pragma clang loop unroll(disable)
+    for (int it = 0; it < ntl; it++) {
+    const int tr = TLOOP ? it : tr0;
+    P1Args a = a0;
+    if (tr) {
+        a.ttf += tr * a.tr.node;
+        a.LO += tr * a.tr.node;
+        a.plus += tr * a.tr.node;
+        a.minus += tr * a.tr.node;
+        a.adf_v += tr * a.tr.lev;
+        a.adf_h += tr * a.tr.edge;
+        if (VERT && !(OPT & 64)) a.del_v += tr * a.tr.node;
+    }
+    if (TLOOP && it > 0) __syncthreads();  // the previous tracer's LDS reads are done
+    // the column's record entries are re-read from LDS per tracer: an opaque copy of j keeps the
+    // compiler from hoisting all 40 of them into registers across the loop (occupancy)
+    int jr = j;
+    if constexpr (TLOOP) asm volatile("" : "+v"(jr));
+    const NodeRec &rec = recs[jr];
     NodeInfo ni{};
-    if (col) ni = recs[j].info;
+    if (col) ni = rec.info;
     const int Ln = ni.Ln;
     const int nw = col ? max(0, min(C, Ln - z0)) : 0;  // wet cells of this thread
     real vx[C], vn[C], p[C], m[C];
@@ -462,7 +479,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
                 vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
             }
         const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
-        cluster_bound<C, RB, ODD>(recs[j].ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
+        cluster_bound<C, RB, ODD>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
         if (no > kRecRing)
             cluster_bound<C, RB, ODD>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn, last1);
         if constexpr ((OPT & 2) && VERT) {
@@ -482,7 +499,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
                 m[c] += RMIN(0., h);
             }
         };
-        for_edges<C, EB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+        for_edges<C, EB, false, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
         if (ne > kRecEdge) for_edges<C, EB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     }
     real *tvx = lds, *tvn = lds + G * L;
@@ -498,7 +515,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
     }
     __syncthreads();
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
-        if (t < kWave) {  // the DMA'd entries (landed: the barrier waited for vmcnt) -> slot offsets
+        if (it == 0 && t < kWave) {  // the DMA'd entries (landed: the barrier waited for vmcnt) -> slot offsets
             const int sl = t < int_n ? (ie_ent[t].w + C - 1) / C : 0;
             int incl = sl;
 #pragma unroll
@@ -608,7 +625,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
                 stv_s<C, true>(const_cast<real *>(a.adf_h) + (size_t)e.x * L + zi, out, nwi);
             }
         }
-        if (na <= 0) return;
+        if (na <= 0) continue;  // (the last statement with barriers is behind)
         if (nw == 0) {  // no wet cell (nlevels_nod2D <= 1): only nz = 1 is limited, from memory
             b = (size_t)ni.n * L + z0;
             ab = (size_t)ni.n * a.nl + z0;
@@ -678,10 +695,19 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, P1Args &a, int G, float
         if constexpr (!(OPT & 64))
             if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
     }
+    }  // tracers
 }
 
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
 __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, float invS)
+{
+    p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
+}
+
+// the tracer-loop form (OPT & 128, tuning build) held to 7 waves/SIMD (it spills there)
+template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT, int OPT, bool ODD = false>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(7))) void k_p1t(MeshPlanDev mp, P1Args a, int G,
+                                                                                       float invS)
 {
     p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
@@ -1376,6 +1402,34 @@ bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 }
 
 #if F2A_TUNING
+// Batched tracers at vlimit 1 in level pairs: one block runs its G columns for every tracer in turn
+// (k_p1t, OPT & 128), XOPT = 64 without c-vertical; FESOM2_P1V_TLOOP=1 (tuning build).  Measured
+// 6 x 1.2M x 80: p1v 15.6 ms against 13.3 ms with a tile per (column group, tracer): the loop keeps
+// the tracer-independent state and the per-tracer pointers live (94 VGPRs, 5 waves/SIMD; bounded to
+// 7 waves it spills).  false: not selected, or not this shape.
+template <int XOPT>
+static bool launch_p1v_tloop(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in, hipError_t *err)
+{
+    const int L = a.nl - 1;
+    const bool odd = odd_pairs(L);
+    if (a.tr.n < 2 || a.vlimit != 1 || !knob("FESOM2_P1V_TLOOP", 0) || !(odd || levels_per_thread(L) == 2)) return false;
+    const int S = (L + 1) / 2, G = group_columns(S);
+    const long groups = (long)(a.n_owned + G - 1) / G;
+    const size_t lds = p1_lds_bytes(G, L, 1, in);
+    const float inv = 1.0f / (float)S;
+    *err = [&]() -> hipError_t {
+        if (odd) {
+            if (in) F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 52 | 128 | XOPT, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 4 | 128 | XOPT, true>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+        if (in) F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 52 | 128 | XOPT>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 4 | 128 | XOPT>), groups, G, S, lds, s, mp, a, G, inv);
+    }();
+    return true;
+}
+#endif
+
+#if F2A_TUNING
 // every measured form of p1v (FESOM2_NT bit 2, FESOM2_P1V_EARLY, FESOM2_NL_PAIR, FESOM2_P1V_INT_DMA)
 static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in)
 {
@@ -1449,6 +1503,8 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
     const bool in = p1v_limits_internal(mp, a);
 #if F2A_TUNING
+    hipError_t err;
+    if (launch_p1v_tloop<0>(mp, a, s, in, &err)) return err;
     return launch_p1v_tuning(mp, a, s, in);
 #else
     const int L = a.nl - 1;
@@ -1500,6 +1556,10 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const bool in = p1v_limits_internal(mp, a);
+#if F2A_TUNING
+    hipError_t err;
+    if (launch_p1v_tloop<64>(mp, a, s, in, &err)) return err;
+#endif
     const int L = a.nl - 1;
     if (odd_pairs(L) && a.vlimit == 1) {
         const int S = (L + 1) / 2, G = group_columns(S);

@@ -131,6 +131,63 @@ void await_stream_(void **s, int *istat)
 
 // ----------------------------------------------------------------------------- phase 1
 
+}  // extern "C"
+
+// The c-vertical fields bound to fct_adf_v (fesom2_bind_c_vertical_), checked alive and large
+// enough for N owned columns; out[] stays null when nothing is bound.  false (reported) on a stale
+// or short binding.
+static bool bound_c_vertical(Buffer *adf_v, int N, int L, int NL, Buffer *out[4])
+{
+    const CvBinding *cv = adf_v->cv;
+    if (!cv) return true;
+    for (int k = 0; k < 4; k++)
+        if (!object_live(cv->b[k], cv->serial[k])) {
+            report("fesom2_bind_c_vertical_: a bound field was freed (bind again)");
+            return false;
+        }
+    const size_t need[4] = {col_bytes(N, L), col_bytes(N, L), col_bytes(N, L), col_bytes(N, NL)};
+    for (int k = 0; k < 4; k++)
+        if (cv->b[k]->size < need[k]) {
+            report("fesom2_bind_c_vertical_: a bound field holds %zu bytes, %zu needed", cv->b[k]->size, need[k]);
+            return false;
+        }
+    for (int k = 0; k < 4; k++) out[k] = cv->b[k];
+    return true;
+}
+
+extern "C" {
+
+void fesom2_bind_c_vertical_(int *istat, void **fct_adf_v, void **del_ttf_advvert, void **hnode, void **hnode_new,
+                             void **area)
+{
+    *istat = 1;
+    Buffer *bv = buf(fct_adf_v, "fct_adf_v");
+    if (!bv) return;
+    void **hs[4] = {del_ttf_advvert, hnode, hnode_new, area};
+    const bool unbind = !(del_ttf_advvert && *del_ttf_advvert) && !(hnode && *hnode) &&
+                        !(hnode_new && *hnode_new) && !(area && *area);
+    if (unbind) {
+        delete bv->cv;
+        bv->cv = nullptr;
+        *istat = 0;
+        return;
+    }
+    static const char *names[4] = {"del_ttf_advvert", "hnode", "hnode_new", "area"};
+    auto *cv = new CvBinding;
+    for (int k = 0; k < 4; k++) {
+        cv->b[k] = buf(hs[k], names[k]);
+        if (!cv->b[k]) {
+            delete cv;
+            return;
+        }
+        cv->serial[k] = cv->b[k]->serial;
+    }
+    delete bv->cv;
+    bv->cv = cv;
+    *istat = 0;
+}
+
+
 void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **fct_ttf_min,
                            void **fct_plus, void **fct_minus, void **ttf, void **fct_LO,
                            void **fct_adf_v, void **fct_adf_h, void **UV_rhs, void **area_inv,
@@ -201,7 +258,22 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
                        "the raw fluxes first)");
                 return;
             }
-            if (!run("fct_ale_p1_b3v", st, [&] { return f2a::launch_p1_b3v(plan->dev, a, st); })) return;
+            Buffer *cvb[4] = {nullptr, nullptr, nullptr, nullptr};
+            if (!bound_c_vertical(badfv, N, L, NL, cvb)) return;
+            if (cvb[0]) {  // c-vertical too (fesom2_bind_c_vertical_)
+                if (has_internal(cvb[0], st)) {
+                    report("fct_ale_pre_comm_acc_: the bound del_ttf_advvert already holds this pass's c-vertical");
+                    return;
+                }
+                a.del_v = dptr<real>(cvb[0]);
+                a.hnode = dptr<real>(cvb[1]);
+                a.hnode_new = dptr<real>(cvb[2]);
+                a.area = dptr<real>(cvb[3]);
+                if (!run("fct_ale_p1v", st, [&] { return f2a::launch_p1v(plan->dev, a, st); })) return;
+                mark_internal(cvb[0], plan, st);
+            } else if (!run("fct_ale_p1_b3v", st, [&] { return f2a::launch_p1_b3v(plan->dev, a, st); })) {
+                return;
+            }
             mark_internal(badfv, plan, st);
             mark_internal(badfh, f2a::p1v_limits_internal(plan->dev, a) ? plan : nullptr, st);
         } else if (!run("fct_ale_p1", st, [&] { return f2a::launch_p1_fused(plan->dev, a, st); })) {
@@ -480,7 +552,17 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
     const Plan *plan = get_plan(mh, N, NT, E, NL, false);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
-    if (kernel_path() != 1 && d.p2_rec && (L % 2 == 0 || L >= 3)) {
+    if (badfv->cv && badfv->cv->b[0] != bdv) {
+        report("fct_ale_c_acc_: del_ttf_advvert is not the one bound to fct_adf_v (fesom2_bind_c_vertical_)");
+        return;
+    }
+    if (has_internal(bdv, st)) {
+        // the fast mode's fct_ale_pre_comm_acc_ did c-vertical already: c-horizontal only
+        f2a::P2Args a{NL, d.p2_rec, N, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dptr<real>(barea), nullptr,
+                      dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
+        if (!run("fct_ale_p2h", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
+        mark_internal(bdv, nullptr, st);
+    } else if (kernel_path() != 1 && d.p2_rec && (L % 2 == 0 || L >= 3)) {
         // fused path: cv + ch in one node kernel over the processing order
         f2a::P2Args a{NL, d.p2_rec, N, nullptr, nullptr, dptr<real>(bttf), dptr<real>(blo), dptr<real>(bh),
                       dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh), dptr<real>(bdv),
@@ -1031,6 +1113,7 @@ void fesom2_free_(void **mem)
     if (!b) return;
     drop_plans_of(b);
     untrack_object(b);
+    delete b->cv;
     (void)hipFree(b->device_pointer);
     if (b->has_event) (void)hipEventDestroy(b->event);
     b->magic = 0;

@@ -147,6 +147,14 @@ class FctAle:
                              d["edges"].ref, d["edge_tri"].ref, dp(self.dt))
         return st.value
 
+    def bind_c_vertical(self, on=True):
+        """fesom2_bind_c_vertical_: in the fast mode (fesom2_set_path_(2)) pre_comm also does
+        c-vertical on this tracer's del_ttf_advvert, and c_step only c-horizontal."""
+        h, st, none = self.h, C.c_int(0), C.c_void_p()
+        refs = [h[k].ref if on else C.byref(none) for k in ("del_v", "hnode", "hnode_new", "area")]
+        dll().fesom2_bind_c_vertical_(C.byref(st), h["adf_v"].ref, *refs)
+        check(st, "fesom2_bind_c_vertical_")
+
     def post_comm_c(self):
         m, h, d = self.m, self.h, self.dm.h
         st = C.c_int(-1)

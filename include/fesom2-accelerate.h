@@ -108,6 +108,15 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
                     int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                     void **nod2D_edges, void **elem2D_edges, real_type *dt);
 
+/* Fast mode (fesom2_set_path_(2)) only: bind the c-step's vertical fields to a tracer's fct_adf_v
+ * once, so that fct_ale_pre_comm_acc_ -- which receives none of them -- also does c-vertical while
+ * its plus/minus, raw fct_adf_v, ttf and fct_LO are in registers; fct_ale_c_acc_ then does
+ * c-horizontal only.  The handles must be the ones later passed to fct_ale_c_acc_ (checked there),
+ * and del_ttf_advvert must hold its pre-c-step value when pre_comm runs (FESOM2 fills it before
+ * fct_ale).  Same results.  Null handles (all four) unbind.  istat 1 on invalid handles/sizes. */
+void fesom2_bind_c_vertical_(int *istat, void **fct_adf_v, void **del_ttf_advvert, void **hnode,
+                             void **hnode_new, void **area);
+
 /* Fused phase 2 = b3-vertical + b3-horizontal + c-vertical + c-horizontal in one node-centric pass
  * (needs fct_plus/minus valid on the halo).  Same results as inter_comm + post_comm + c; alg_state -> 9. */
 void fct_ale_post_comm_c_acc_(int *alg_state, void **s, void **fct_plus, void **fct_minus,

@@ -605,10 +605,12 @@ def test_graph_replay_matches_oracle():
 @pytest.mark.parametrize("resident", [True, False])
 @pytest.mark.parametrize("internal", ["0", "1"])
 @pytest.mark.parametrize("vlimit", [1, 2])
-def test_reference_sequence_fast_mode(name, full, resident, internal, vlimit, monkeypatch):
+@pytest.mark.parametrize("bind", [False, True])
+def test_reference_sequence_fast_mode(name, full, resident, internal, vlimit, bind, monkeypatch):
     """fesom2_set_path_(2): the unmodified reference sequence pre_comm -> inter_comm -> post_comm -> c
-    with b3v (and the block-internal edges) done inside pre_comm; every output exact, with the
-    reference's transfer semantics too (inter_comm still hands the host the limited fct_adf_v)."""
+    with b3v (and the block-internal edges) done inside pre_comm -- and with c-vertical bound
+    (fesom2_bind_c_vertical_) also cv there, the c-step c-horizontal only; every output exact, with
+    the reference's transfer semantics too (inter_comm still hands the host the limited fct_adf_v)."""
     monkeypatch.setenv("FESOM2_P1V_B3H", internal)
     m, f = mesh(name, full)
     st, p1 = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
@@ -617,6 +619,8 @@ def test_reference_sequence_fast_mode(name, full, resident, internal, vlimit, mo
     abi.set_path("reference")
     dm = engine.DeviceMesh(m)
     e = engine.FctAle(dm, f, vlimit=vlimit)
+    if bind:
+        e.bind_c_vertical()
     pristine = {k: e.host[k].copy() for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")}
     try:
         for _ in range(2):  # twice on the same buffers: the marks are consumed every pass
@@ -649,6 +653,38 @@ def test_fast_mode_marks_refuse_other_phase_2():
         assert e.pre_comm() == 6, abi.last_error()
         assert e.post_comm_c() != 9 and "fct_adf_v" in abi.last_error()
         assert e.pre_comm() != 6 and "upload" in abi.last_error()
+    finally:
+        abi.set_path("fused")
+        e.free()
+        dm.free()
+
+
+def test_fast_mode_c_vertical_binding_checks():
+    """A bound del_ttf_advvert that the c-step is not given is refused; unbinding restores the
+    b3v-only pre_comm (and the full c-step)."""
+    m, f = mesh("8k x 20")
+    want = O.full_pass(m, f)
+    abi.set_path("reference")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        e.bind_c_vertical()
+        assert e.pre_comm() == 6 and e.inter_comm() == 7 and e.post_comm() == 8
+        h = e.h
+        e.h = dict(h, del_v=h["del_h"])  # the wrong del_ttf_advvert handle
+        assert e.c_step() != 9 and "bound" in abi.last_error()
+        e.h = h
+        assert e.c_step() == 9, abi.last_error()
+        e.sync()
+        for k in ("del_v", "del_h", "adf_v", "adf_h"):
+            assert np.array_equal(e.download(k), want[k]), k
+        e.bind_c_vertical(False)
+        for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(k)
+        assert e.full_pass(fused=False) == 9, abi.last_error()
+        e.sync()
+        for k in ("del_v", "del_h", "adf_v", "adf_h"):
+            assert np.array_equal(e.download(k), want[k]), k
     finally:
         abi.set_path("fused")
         e.free()

@@ -65,10 +65,10 @@ __device__ __forceinline__ int xcd_tile(int b, int G)
 
 // p1v's shape: block = G columns x S = L/2 slots; node columns n*L, stride-nl arrays n*(L+1),
 // adf_h: three edge columns per node (edge e = 3n + k, column e*L)
-__global__ __launch_bounds__(1024) void k_cols(Arrays a, int nodes, int L, int G)
+__global__ __launch_bounds__(1024) void k_cols(Arrays a, int nodes, int L, int G, int swz = 1)
 {
     const int S = L / 2, t = threadIdx.x, j = t / S, u = t - j * S;
-    const int n = xcd_tile(blockIdx.x, gridDim.x) * G + j;
+    const int n = (swz ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x) * G + j;
     if (j >= G || n >= nodes) return;
     const int z0 = 2 * u, nl = L + 1;
     const size_t b = (size_t)n * L + z0, ab = (size_t)n * nl + z0;
@@ -150,6 +150,12 @@ int main(int argc, char **argv)
             hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G);
         });
         if (G == 8) cols_tbs = r;
+    }
+    if (!json) {  // the same without the XCD-contiguous tile ranges (block b -> tile b)
+        const int G = 8, thr = ((G * (L / 2) + 63) / 64) * 64;
+        timeit("cols G=8 no XCD swizzle", bytes_p1, [&] {
+            hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G, 0);
+        });
     }
     if (json)
         printf("{\"copy_GBps\": %.1f, \"p1v_pattern_GBps\": %.1f, \"nodes\": %ld, \"levels\": %d}\n", copy_tbs * 1e3,
