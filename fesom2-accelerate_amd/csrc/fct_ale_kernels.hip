@@ -704,6 +704,15 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
 
+// p1 held to W waves/SIMD (amdgpu_waves_per_eu): the register allocator trades a few spills for
+// occupancy where a form sits just above a VGPR step (65 VGPRs = 7 waves, 74 = 6)
+template <int W, int VLIMIT, int C, int RB, int EB, bool NT, bool VERT, int OPT, bool ODD = false>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(W))) void k_p1o(MeshPlanDev mp, P1Args a, int G,
+                                                                                       float invS)
+{
+    p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
+}
+
 // the tracer-loop form (OPT & 128, tuning build) held to 7 waves/SIMD (it spills there)
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT, int OPT, bool ODD = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(7))) void k_p1t(MeshPlanDev mp, P1Args a, int G,
@@ -1505,6 +1514,28 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #if F2A_TUNING
     hipError_t err;
     if (launch_p1v_tloop<0>(mp, a, s, in, &err)) return err;
+    // FESOM2_P1V_WAVES = W: the production forms held to W waves/SIMD
+    if (const int W = knob("FESOM2_P1V_WAVES", 0); W >= 6 && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = group_columns(S);
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const size_t lds = p1_lds_bytes(G, L, 1, in);
+            const float inv = 1.0f / (float)S;
+#define F2A_P1O(WW)                                                                                                     \
+            if (W == WW) {                                                                                            \
+                if (odd && in) F2A_LAUNCH_GROUPS((k_p1o<WW, 1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv); \
+                if (odd) F2A_LAUNCH_GROUPS((k_p1o<WW, 1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);      \
+                if (in) F2A_LAUNCH_GROUPS((k_p1o<WW, 1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, a, G, inv);             \
+                F2A_LAUNCH_GROUPS((k_p1o<WW, 1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, inv);                      \
+            }
+            F2A_P1O(6)
+            F2A_P1O(7)
+            F2A_P1O(8)
+#undef F2A_P1O
+        }
+    }
     return launch_p1v_tuning(mp, a, s, in);
 #else
     const int L = a.nl - 1;

@@ -107,7 +107,11 @@ int main(int argc, char **argv)
         ms /= reps;
         return (ro ? rbytes : bytes) / (ms * 1e-3) / 1e12;
     };
-    {  // separate hipMallocs (the engine's layout)
+    const int trials = argc > 3 ? atoi(argv[3]) : 1;
+    for (int trial = 0; trial < trials; trial++) {  // separate hipMallocs (the engine's layout)
+        // a spacer of a different size each trial: the arrays land on other physical pages
+        void *spacer = nullptr;
+        if (trial) CHECK(hipMalloc(&spacer, (size_t)trial * 37 * 1048576 + 4096));
         double *p[11];
         for (int k = 0; k < 11; k++) {
             CHECK(hipMalloc(&p[k], sz[k] * sizeof(double)));
@@ -124,7 +128,31 @@ int main(int argc, char **argv)
         const double rw = timeit(a, false), ro = timeit(a, true);
         printf("%-24s 11R+4W %6.2f TB/s   11R %6.2f TB/s\n", "separate hipMalloc", rw, ro);
         for (int k = 0; k < 11; k++) CHECK(hipFree(p[k]));
+        if (spacer) CHECK(hipFree(spacer));
     }
+    for (int trial = 0; trial < trials; trial++) {  // one pool, arrays back to back + k * 4352 B
+        void *spacer = nullptr;
+        if (trial) CHECK(hipMalloc(&spacer, (size_t)trial * 37 * 1048576 + 4096));
+        long total = 0;
+        for (int k = 0; k < 11; k++) total += ((sz[k] * 8 + 2097151) / 2097152) * 2097152 + 4352;
+        char *pool;
+        CHECK(hipMalloc(&pool, total));
+        CHECK(hipMemset(pool, 0, total));
+        double *p[11];
+        long off = 0;
+        for (int k = 0; k < 11; k++) {
+            p[k] = reinterpret_cast<double *>(pool + off + k * 4352);
+            off += ((sz[k] * 8 + 2097151) / 2097152) * 2097152;
+        }
+        Arrays a;
+        assign(a, p);
+        const double rw = timeit(a, false), ro = timeit(a, true);
+        printf("%-24s 11R+4W %6.2f TB/s   11R %6.2f TB/s\n", "pool trial", rw, ro);
+        fflush(stdout);
+        CHECK(hipFree(pool));
+        if (spacer) CHECK(hipFree(spacer));
+    }
+    if (trials > 1) return 0;
     const long pads[] = {0, 256, 4096, 12544, 65536, 262144, 1048576, 3 * 1048576 + 4352};
     long total = 0;
     for (int k = 0; k < 11; k++) total += ((sz[k] * 8 + 2097151) / 2097152) * 2097152;

@@ -82,6 +82,61 @@ __global__ __launch_bounds__(1024) void k_cols(Arrays a, int nodes, int L, int G
     st(a.dv_o + b, s + h);
 }
 
+// odd L as p1v runs it: S = (L+1)/2 slots, the last slot holds one level (its pair load starts a
+// level early, inside the column).  `stride` = doubles between columns of the L-stride arrays
+// (L: the ABI layout; L+1: padded, every column 16-byte aligned).  align = 1: parity-aware pairing
+// of the L-stride arrays -- a column starting at 8 mod 16 gets its single-level slot first, so all
+// its pair loads are 16-byte aligned (the stride-nl arrays keep the plain pairing).
+__device__ __forceinline__ d2 ld2(const double *p, bool single_hi, bool single_lo)
+{
+    if (single_lo) return d2{p[0], 0.0};
+    return single_hi ? d2{0.0, p[1]} : ld(p);
+}
+
+__global__ __launch_bounds__(1024) void k_cols_odd(Arrays a, int nodes, int L, int G, int stride, int align)
+{
+    const int S = (L + 1) / 2, t = threadIdx.x, j = t / S, u = t - j * S;
+    const int n = xcd_tile(blockIdx.x, gridDim.x) * G + j;
+    if (j >= G || n >= nodes) return;
+    const int nl = L + 1;
+    const size_t col = (size_t)n * stride;
+    const bool shifted = align && (col & 1);
+    // L-stride arrays: plain pairs (2u, 2u+1), last slot = (L-2, L-1) taking the second; shifted:
+    // slot 0 = level 0 alone, slot u = (2u-1, 2u)
+    int zl;
+    bool hi = false, lo = false;
+    if (!shifted) {
+        zl = 2 * u;
+        if (zl + 1 == L) {
+            zl -= 1;
+            hi = true;
+        }
+    } else {
+        zl = u == 0 ? 0 : 2 * u - 1;
+        lo = u == 0;
+    }
+    int zn = 2 * u;  // stride-nl arrays: plain pairs, the last one at L-1 (nl = L+1 holds it)
+    const size_t b = col + zl, ab = (size_t)n * nl + zn;
+    d2 s = ld2(a.ttf + b, hi, lo) + ld2(a.LO + b, hi, lo) + ld(a.adfv + ab) + ld(a.ainv + ab) + ld(a.area + ab) +
+           ld2(a.hn + b, hi, lo) + ld2(a.hnn + b, hi, lo) + ld2(a.dv + b, hi, lo);
+    const size_t e = (size_t)3 * col + zl;
+    d2 h = ld2(a.adfh + e, hi, lo) + ld2(a.adfh + e + stride, hi, lo) + ld2(a.adfh + e + 2 * stride, hi, lo);
+    if (lo) {
+        a.plus[b] = s.x;
+        a.minus[b] = h.x;
+        a.dv_o[b] = s.x + h.x;
+    } else if (hi) {
+        a.plus[b + 1] = s.y;
+        a.minus[b + 1] = h.y;
+        a.dv_o[b + 1] = s.y + h.y;
+    } else {
+        st(a.plus + b, s);
+        st(a.minus + b, h);
+        st(a.dv_o + b, s + h);
+    }
+    st(a.adfv_o + ab, s - h);
+}
+
 int main(int argc, char **argv)
 {
     const long nodes = argc > 1 ? atol(argv[1]) : 1200000;
@@ -98,17 +153,17 @@ int main(int argc, char **argv)
         return p;
     };
     Arrays a;
-    a.ttf = alloc(cn);
-    a.LO = alloc(cn);
+    a.ttf = alloc(cnl);  // room for the padded-stride variant
+    a.LO = alloc(cnl);  // room for the padded-stride variant
     a.adfv = alloc(cnl);
     a.ainv = alloc(cnl);
     a.area = alloc(cnl);
-    a.hn = alloc(cn);
-    a.hnn = alloc(cn);
-    a.dv = alloc(cn);
-    a.adfh = alloc(3 * cn);
-    a.plus = alloc(cn);
-    a.minus = alloc(cn);
+    a.hn = alloc(cnl);  // room for the padded-stride variant
+    a.hnn = alloc(cnl);  // room for the padded-stride variant
+    a.dv = alloc(cnl);  // room for the padded-stride variant
+    a.adfh = alloc(3 * cnl);
+    a.plus = alloc(cnl);  // room for the padded-stride variant
+    a.minus = alloc(cnl);  // room for the padded-stride variant
     a.adfv_o = const_cast<double *>(a.adfv);  // in place, as p1v
     a.dv_o = const_cast<double *>(a.dv);
     double *src = alloc(4 * cn), *dst = alloc(4 * cn);
@@ -150,6 +205,17 @@ int main(int argc, char **argv)
             hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G);
         });
         if (G == 8) cols_tbs = r;
+    }
+    if (!json && L % 2 == 1) {  // odd L: p1v's slot shape, ABI stride vs padded vs parity-aware pairs
+        const int G = 8, S = (L + 1) / 2, thr = ((G * S + 63) / 64) * 64;
+        for (int mode = 0; mode < 3; mode++) {
+            const char *nm[3] = {"odd cols stride L", "odd cols stride L+1", "odd cols aligned pairs"};
+            const int stride = mode == 1 ? L + 1 : L;
+            timeit(nm[mode], bytes_p1, [&] {
+                hipLaunchKernelGGL(k_cols_odd, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L,
+                                   G, stride, mode == 2 ? 1 : 0);
+            });
+        }
     }
     if (!json) {  // the same without the XCD-contiguous tile ranges (block b -> tile b)
         const int G = 8, thr = ((G * (L / 2) + 63) / 64) * 64;
