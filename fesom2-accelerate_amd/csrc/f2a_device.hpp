@@ -126,6 +126,23 @@ __device__ __forceinline__ void slot_of(int t, int S, float invS, int &j, int &u
 
 __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
 
+// XCD-chunked tracer tiles: XCD x (blocks b with b % 8 == x, dispatched round-robin) owns column
+// groups [x*gx, (x+1)*gx), gx = ceil(groups/8), and walks them in chunks of K groups, each chunk
+// once per tracer -- the tracers' passes over a chunk follow each other, so each keeps the
+// single-tracer reuse distance of the neighbour gathers, and the chunk's records and mesh fields
+// come back from L2 / the Infinity Cache for the later tracers.  Grid: 8 * gx * ntr blocks;
+// returns -1 for the padding tiles past the last group.
+__device__ __forceinline__ int group_tracer_chunked(int ntr, int groups, int K, int &tr)
+{
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int gx = (groups + 7) >> 3, span = K * ntr;
+    const int c = k / span, r = k - c * span;
+    const int kc = min(K, gx - c * K);
+    tr = r / kc;
+    const int g = x * gx + c * K + (r - tr * kc);
+    return g < groups ? g : -1;
+}
+
 // tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
 // for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
 // keep the L2 to themselves)

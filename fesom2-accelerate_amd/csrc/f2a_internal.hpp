@@ -182,6 +182,7 @@ struct MeshPlanDev {
 struct Tracers {
     int n = 1;
     size_t node = 0, lev = 0, edge = 0;
+    int chunk = 0;  // p1v: > 0 = XCD-chunked tracer tiles of that many column groups (group_tracer_chunked)
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().

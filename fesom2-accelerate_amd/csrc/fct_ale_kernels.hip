@@ -331,7 +331,11 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
     int tr0 = 0;
-    const int first = (TLOOP ? block_tile() : group_tracer(a0.tr.n, tr0, c_tracer_major & 1)) * G;
+    const int grp = TLOOP ? block_tile()
+                    : a0.tr.chunk > 0 ? group_tracer_chunked(a0.tr.n, (a0.n_owned + G - 1) / G, a0.tr.chunk, tr0)
+                                      : group_tracer(a0.tr.n, tr0, c_tracer_major & 1);
+    if (grp < 0) return;  // a padding tile of the chunked grid (block-uniform, before any barrier)
+    const int first = grp * G;
     const int ntl = TLOOP ? a0.tr.n : 1;
     const int ncol = min(G, a0.n_owned - first);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
@@ -1514,6 +1518,24 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #if F2A_TUNING
     hipError_t err;
     if (launch_p1v_tloop<0>(mp, a, s, in, &err)) return err;
+    // FESOM2_TRACER_CHUNK = K: batched tracers in XCD-chunked tiles of K column groups
+    if (const int K = knob("FESOM2_TRACER_CHUNK", 0); K > 0 && a.tr.n > 1 && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            P1Args b = a;
+            b.tr.chunk = K;
+            const int S = (L + 1) / 2, G = group_columns(S);
+            const long gx = ((long)(a.n_owned + G - 1) / G + 7) / 8;
+            const long groups = 8 * gx * a.tr.n;
+            const size_t lds = p1_lds_bytes(G, L, 1, in);
+            const float inv = 1.0f / (float)S;
+            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, b, G, inv);
+            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, b, G, inv);
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, b, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, b, G, inv);
+        }
+    }
     // FESOM2_P1V_WAVES = W: the production forms held to W waves/SIMD
     if (const int W = knob("FESOM2_P1V_WAVES", 0); W >= 6 && a.vlimit == 1) {
         const int L = a.nl - 1;

@@ -16,13 +16,16 @@
 !         post_comm -> c; results land in the bound host arrays)
 ! mode 1: device resident, direction-split pass (pre_comm_v -> post_comm_h), results downloaded
 ! mode 2: as 1, the pass captured into a hipGraph (fesom2_graph_*) after one eager pass, replayed
+! mode 3: mode 0's unmodified sequence and transfer semantics in the fast mode: fesom2_set_path_(2)
+!         and fesom2_bind_c_vertical_ once before the step (b3v, cv and the block-internal edges
+!         inside pre_comm, c-horizontal alone in the c-step)
 ! OUT: int32(4) alg_states, then fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert,
 !      del_ttf_advhoriz in the IN format.
 program fct_ale_host
   use iso_c_binding
   use fesom2_accelerate
   implicit none
-  integer(c_int) :: hdr(8), N, H, T, E, nl, dim, vlimit, mode, NT, L, istat, st(4), zero, one, ntr
+  integer(c_int) :: hdr(8), N, H, T, E, nl, dim, vlimit, mode, NT, L, istat, st(4), zero, one, two, ntr
   integer(c_int), allocatable, target :: nlev_nod(:), nlev_elem(:), elem_nodes(:), nie_num(:), nie(:), &
                                          edges(:), edge_tri(:)
   real(c_double), allocatable, target :: ttf(:), lo(:), adf_v(:), adf_h(:), area(:), area_inv(:), hnode(:), &
@@ -48,13 +51,13 @@ program fct_ale_host
   close(u)
   allocate(plus(NT * L), minus(NT * L))
   plus = 0; minus = 0
-  yes = .true.; no = .false.; zero = 0; one = 1; ntr = 1; st = -1
+  yes = .true.; no = .false.; zero = 0; one = 1; two = 2; ntr = 1; st = -1
   nullh = c_null_ptr
 
   call set_mpi_rank(zero, one)
   call make_stream(s, istat)
   call check(istat, "make_stream")
-  if (mode >= 1) call fesom2_set_resident(one)
+  if (mode == 1 .or. mode == 2) call fesom2_set_resident(one)
   ! mesh: once per run (reference .cu:114-127)
   call upload_mesh(h_nlev_nod, nlev_nod); call upload_mesh(h_nlev_elem, nlev_elem)
   call upload_mesh(h_elem_nodes, elem_nodes); call upload_mesh(h_nie_num, nie_num)
@@ -72,7 +75,12 @@ program fct_ale_host
   call transfer_var_async(h_adf_v, adf_v, s, yes)
   call transfer_var_async(h_adf_h, adf_h, s, yes)
 
-  if (mode == 0) then
+  if (mode == 3) then
+    call fesom2_set_path(two)
+    call fesom2_bind_c_vertical(istat, h_adf_v, h_del_v, h_hnode, h_hnode_new, h_area)
+    call check(istat, "fesom2_bind_c_vertical")
+  end if
+  if (mode == 0 .or. mode == 3) then
     call fct_ale_pre_comm_acc(st(1), s, h_tmax, h_tmin, h_plus, h_minus, h_ttf, h_lo, h_adf_v, h_adf_h, h_uv, &
         h_area_inv, N, H, T, E, nl, h_nlev_nod, h_nlev_elem, h_elem_nodes, h_nie_num, h_nie, dim, h_edges, &
         h_edge_tri, vlimit, sc(2), sc(3), sc(1))

@@ -112,6 +112,18 @@ module fesom2_accelerate
       import :: c_int
       integer(c_int) :: resident
     end subroutine
+    ! kernel path: 0 fused, 1 stepwise, 2 the reference sequence's fast mode
+    subroutine fesom2_set_path(path) bind(C, name="fesom2_set_path_")
+      import :: c_int
+      integer(c_int) :: path
+    end subroutine
+    ! fast mode: c-vertical inside fct_ale_pre_comm_acc_ (the c-step's vertical fields bound once)
+    subroutine fesom2_bind_c_vertical(istat, fct_adf_v, del_ttf_advvert, hnode, hnode_new, area) &
+        bind(C, name="fesom2_bind_c_vertical_")
+      import :: c_ptr, c_int
+      integer(c_int) :: istat
+      type(c_ptr) :: fct_adf_v, del_ttf_advvert, hnode, hnode_new, area
+    end subroutine
     subroutine fesom2_download(handle, host, istat) bind(C, name="fesom2_download_")
       import :: c_ptr, c_double, c_int
       type(c_ptr) :: handle

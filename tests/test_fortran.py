@@ -71,7 +71,8 @@ def test_fortran_host_builds_and_binds_the_abi():
     exported = {ln.split()[-1] for ln in exported.splitlines() if ln.split()}
     assert len(used) >= 16 and used <= exported, used - exported
     for name in ("fct_ale_pre_comm_acc_", "fct_ale_inter_comm_acc_", "fct_ale_post_comm_acc_", "fct_ale_c_acc_",
-                 "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_", "fesom2_graph_begin_", "fesom2_graph_launch_"):
+                 "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_", "fesom2_graph_begin_", "fesom2_graph_launch_",
+                 "fesom2_set_path_", "fesom2_bind_c_vertical_"):
         assert name in used
 
 
@@ -88,7 +89,8 @@ def test_input_format_header(tmp_path):
 
 @pytest.mark.gpu
 @needs_flang
-@pytest.mark.parametrize("mode", [0, 1, 2], ids=["reference_sequence", "resident_split", "graph_replay"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3], ids=["reference_sequence", "resident_split", "graph_replay",
+                                                  "reference_sequence_fast_mode"])
 @pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
 def test_fortran_host_matches_oracle(tmp_path, mode, name):
     import oracle as O
@@ -99,7 +101,7 @@ def test_fortran_host_matches_oracle(tmp_path, mode, name):
     r = subprocess.run([HOST, str(fin), str(fout)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     states, got = read_output(fout)
-    assert states == ([6, 7, 8, 9] if mode == 0 else [7, 9, -1, -1]), states  # mode 2: the captured calls
+    assert states == ([6, 7, 8, 9] if mode in (0, 3) else [7, 9, -1, -1]), states  # mode 2: the captured calls
     want = O.full_pass(m, f)
     assert_cols_equal(got["plus"], want["plus"], m.nlev_nod, m.L, m.N, "fct_plus")
     assert_cols_equal(got["minus"], want["minus"], m.nlev_nod, m.L, m.N, "fct_minus")
