@@ -347,6 +347,12 @@ def main():
                     help="(default) after timing, rerun one pass on pristine inputs and compare every owned cell and "
                          "local edge with the oracle on each rank's local mesh; the line carries \"check\" and the "
                          "exit status is 1 on any mismatch")
+    ap.add_argument("--kernel-timing", default="dominant", choices=["all", "dominant", "none"],
+                    help="HIP events in the timed region around the dominant kernel only (default: the split "
+                         "pass's p1v; every other path times every launch), around every launch (all), or none "
+                         "(no roofline).  Each timed launch adds two events to the stream: at 127k x 47 timing "
+                         "every launch costs 5 %% of the pass.  With 'dominant' the other kernels are timed on "
+                         "a few extra steps after the timed region")
     ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity check")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
                     help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "
@@ -527,7 +533,8 @@ def main():
         abi.device_sync()
 
     # ---- timed region: exactly K steps, barrier + device sync on both sides
-    abi.kernel_timing(not args.graph)
+    abi.kernel_timing(not args.graph and args.kernel_timing != "none")
+    abi.kernel_timing_only("fct_ale_p1v" if args.kernel_timing == "dominant" and args.path == "split" else None)
     abi.kernel_timing_reset()
     barrier()
     abi.device_sync()
@@ -544,6 +551,19 @@ def main():
     wall = t1 - t0
     gpu_ms = ev0.elapsed_ms(ev1)
     stats = abi.kernel_stats()
+    timed_only = args.kernel_timing == "dominant" and args.path == "split" and not args.graph
+    breakdown = {}
+    if timed_only:
+        # the per-kernel breakdown, outside the timed region: a few more steps with every launch timed
+        # (every rank runs them: the N > 1 step contains the exchange)
+        abi.kernel_timing_only(None)
+        abi.kernel_timing(True)
+        abi.kernel_timing_reset()
+        for _ in range(min(args.steps, 10)):
+            step()
+        abi.device_sync()
+        abi.kernel_timing(False)
+        breakdown = abi.kernel_stats()
 
     if dist is not None:
         import torch
@@ -564,9 +584,10 @@ def main():
     s.update(mesh_info)
     kb = kernel_bytes(s, args.tracers, split=args.path in ("split", "reference"))
     per_kernel = {}
-    for name, (cnt, tot) in stats.items():
+    for name, (cnt, tot) in list(stats.items()) + [kv for kv in breakdown.items() if kv[0] not in stats]:
         avg = tot / max(cnt, 1)
-        entry = {"launches": cnt, "avg_ms": round(avg, 4)}
+        entry = {"launches": cnt, "avg_ms": round(avg, 4),
+                 "timed": "timed region" if name in stats else "extra steps after the timed region"}
         if name in kb:
             entry["alg_bytes"] = kb[name]
             entry["GBps"] = round(kb[name] / (avg * 1e-3) / 1e9, 1)

@@ -193,6 +193,7 @@ struct TimedLaunch {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 bool g_timing = false;
+std::string g_timing_only;  // fesom2_kernel_timing_only_: time only launches of this name (empty: all)
 std::mutex g_tmutex;
 std::vector<TimedLaunch *> g_pending;
 struct Acc {
@@ -218,7 +219,12 @@ void resolve_pending()
 }
 }  // namespace
 
-bool timing_enabled() { return g_timing; }
+bool timing_enabled(const char *name)
+{
+    if (!g_timing) return false;
+    std::lock_guard<std::mutex> lock(g_tmutex);
+    return g_timing_only.empty() || g_timing_only == name;
+}
 
 // ----------------------------------------------------------------------------- live objects
 
@@ -470,6 +476,12 @@ void fesom2_kernel_timing_(int *on)
     std::lock_guard<std::mutex> lock(f2a::g_tmutex);
     f2a::resolve_pending();
     f2a::g_timing = on && *on;
+}
+
+void fesom2_kernel_timing_only_(const char *name)
+{
+    std::lock_guard<std::mutex> lock(f2a::g_tmutex);
+    f2a::g_timing_only = name ? name : "";
 }
 
 void fesom2_kernel_timing_reset_(void)

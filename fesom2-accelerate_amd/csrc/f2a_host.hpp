@@ -110,7 +110,7 @@ bool defer_event_wait(Buffer *b, hipStream_t s);
 
 // ---- per-kernel timing (fesom2_kernel_timing_): HIP events recorded around each launch on the
 //      launch stream while enabled; resolved when the statistics are read.
-bool timing_enabled();
+bool timing_enabled(const char *name);
 void timing_begin(const char *name, hipStream_t s, void **token);
 void timing_end(void *token, hipStream_t s);
 // Launch through `f` with optional timing; reports failures under `name`.
@@ -118,7 +118,7 @@ template <class F>
 bool run(const char *name, hipStream_t s, F &&f)
 {
     void *tok = nullptr;
-    if (timing_enabled() && !capturing(s)) timing_begin(name, s, &tok);
+    if (timing_enabled(name) && !capturing(s)) timing_begin(name, s, &tok);
     const bool good = ok(f(), name);
     if (tok) timing_end(tok, s);
     return good;

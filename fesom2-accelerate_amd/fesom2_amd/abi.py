@@ -24,7 +24,7 @@ EXPORTS = (
     "fesom2_prepare_mesh_", "fesom2_download_", "fesom2_upload_", "fesom2_free_", "fesom2_free_stream_",
     "fesom2_free_pinned_", "fesom2_device_sync_", "fesom2_last_error", "fesom2_event_create_",
     "fesom2_event_record_", "fesom2_event_elapsed_", "fesom2_event_free_",
-    "fesom2_kernel_timing_", "fesom2_kernel_timing_reset_", "fesom2_kernel_stats_",
+    "fesom2_kernel_timing_", "fesom2_kernel_timing_only_", "fesom2_kernel_timing_reset_", "fesom2_kernel_stats_",
     "fesom2_comm_unique_id_", "fesom2_comm_init_", "fesom2_comm_free_", "fesom2_comm_info_", "fesom2_halo_plan_",
     "fesom2_halo_plan_free_", "fct_ale_exchange_acc_", "fct_ale_exchange_post_comm_c_acc_",
     "fct_ale_pre_comm_batched_acc_", "fct_ale_post_comm_c_batched_acc_", "fct_ale_exchange_batched_acc_",
@@ -221,6 +221,11 @@ def device_sync():
 def kernel_timing(on):
     """Enable/disable per-launch HIP-event timing inside the library."""
     dll().fesom2_kernel_timing_(ip(1 if on else 0))
+
+
+def kernel_timing_only(name=None):
+    """Time only the launches called ``name`` (None: every launch)."""
+    dll().fesom2_kernel_timing_only_(name.encode() if name else None)
 
 
 def kernel_timing_reset():

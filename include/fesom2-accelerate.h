@@ -188,6 +188,9 @@ const char *fesom2_last_error(void);
  * fesom2_kernel_stats_ writes "name count total_ms" lines (NUL-terminated, truncated to *len bytes)
  * and sets *len to the size needed. */
 void fesom2_kernel_timing_(int *on);
+/* Restrict the timing to launches named `name` (NULL or "": every launch).  Each timed launch adds
+ * two events on its stream; timing one kernel keeps the others' boundaries free of them. */
+void fesom2_kernel_timing_only_(const char *name);
 void fesom2_kernel_timing_reset_(void);
 void fesom2_kernel_stats_(char *buf, int *len);
 /* Timing: create/record/elapsed on a stream (HIP events); used by the benchmark harness. */
