@@ -689,3 +689,34 @@ def test_fast_mode_c_vertical_binding_checks():
         abi.set_path("fused")
         e.free()
         dm.free()
+
+
+def test_kernel_timing_only_times_the_named_kernel():
+    """fesom2_kernel_timing_only_ (bench.py --kernel-timing dominant): while a name is set only that
+    kernel's launches get events; with None every launch of the split pass is timed again.  Results
+    are unaffected by the timing."""
+    m, f = mesh("8k x 20", full_depth=True)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f, copy=False)
+    try:
+        abi.kernel_timing(True)
+        for only, want in (("fct_ale_p1v", {"fct_ale_p1v"}), (None, {"fct_ale_p1v", "fct_ale_b3_horizontal", "fct_ale_p2h"})):
+            abi.kernel_timing_only(only)
+            abi.kernel_timing_reset()
+            for _ in range(3):
+                for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+                    e.upload(k)  # pristine inputs for every pass
+                assert e.split_pass() == 9, abi.last_error()
+            e.sync()
+            st = abi.kernel_stats()
+            assert set(st) == want, st
+            assert all(cnt == 3 and ms > 0 for cnt, ms in st.values()), st
+        got = {k: e.download(k) for k in ("adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        abi.kernel_timing(False)
+        abi.kernel_timing_only(None)
+        e.free()
+        dm.free()
+    want = O.full_pass(m, f)
+    for k, g in got.items():
+        assert np.array_equal(g, want[k]), k
