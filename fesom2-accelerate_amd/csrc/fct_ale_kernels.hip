@@ -1536,6 +1536,31 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, b, G, inv);
         }
     }
+    // FESOM2_P1V_BATCH = 10*RB + EB: the production forms with other gather batches (cluster nodes /
+    // edges per round trip; 22 = the product's)
+    if (const int B = knob("FESOM2_P1V_BATCH", 22); B != 22 && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = group_columns(S);
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const size_t lds = p1_lds_bytes(G, L, 1, in);
+            const float inv = 1.0f / (float)S;
+#define F2A_P1B(RB, EB)                                                                                                        \
+            if (B == 10 * RB + EB) {                                                                                          \
+                if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, RB, EB, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv); \
+                if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, RB, EB, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);      \
+                if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, RB, EB, true, true, 52>), groups, G, S, lds, s, mp, a, G, inv);             \
+                F2A_LAUNCH_GROUPS((k_p1<1, 2, RB, EB, true, true, 4>), groups, G, S, lds, s, mp, a, G, inv);                      \
+            }
+            F2A_P1B(3, 3)
+            F2A_P1B(3, 2)
+            F2A_P1B(2, 3)
+            F2A_P1B(6, 2)
+            F2A_P1B(2, 6)
+#undef F2A_P1B
+        }
+    }
     // FESOM2_P1V_WAVES = W: the production forms held to W waves/SIMD
     if (const int W = knob("FESOM2_P1V_WAVES", 0); W >= 6 && a.vlimit == 1) {
         const int L = a.nl - 1;
