@@ -27,12 +27,24 @@ static __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measur
 static __constant__ int c_ablate = 0;
 // FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile order
 static __constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
+// FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range backwards, so it
+// starts on the data the previous kernel touched last (still in the Infinity Cache)
+static __constant__ int c_tile_rev = 0;
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
 {
     if (!c_xcd_swizzle) return b;
     const int q = G >> 3, r = G & 7, x = b & 7, k = b >> 3;
     return x * q + (x < r ? x : r) + k;
+}
+
+// the same ranges, each walked from its end (bijective: XCD x has q + (x < r) tiles)
+__device__ __forceinline__ int xcd_tile_rev(int b, int G)
+{
+    if (!c_xcd_swizzle) return G - 1 - b;
+    const int q = G >> 3, r = G & 7, x = b & 7, k = b >> 3;
+    const int len = q + (x < r ? 1 : 0);
+    return x * q + (x < r ? x : r) + (len - 1 - k);
 }
 
 // the tuning build's knobs of the __constant__ switches above (the product keeps the defaults)
@@ -50,6 +62,8 @@ static void init_swizzle()
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_major), &v, sizeof v);
     if (const int v = knob("FESOM2_ABLATE", 0); v != 0)
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ablate), &v, sizeof v);
+    if (const int v = knob("FESOM2_TILE_REV", 0); v != 0)
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tile_rev), &v, sizeof v);
 #endif
 }
 
@@ -146,9 +160,9 @@ __device__ __forceinline__ int group_tracer_chunked(int ntr, int groups, int K, 
 // tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
 // for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
 // keep the L2 to themselves)
-__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false)
+__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false, bool rev = false)
 {
-    const int t = block_tile();
+    const int t = rev ? xcd_tile_rev(blockIdx.x, gridDim.x) : block_tile();
     if (ntr == 1) {
         tr = 0;
         return t;

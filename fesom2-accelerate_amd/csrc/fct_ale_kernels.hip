@@ -333,7 +333,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     int tr0 = 0;
     const int grp = TLOOP ? block_tile()
                     : a0.tr.chunk > 0 ? group_tracer_chunked(a0.tr.n, (a0.n_owned + G - 1) / G, a0.tr.chunk, tr0)
-                                      : group_tracer(a0.tr.n, tr0, c_tracer_major & 1);
+                                      : group_tracer(a0.tr.n, tr0, c_tracer_major & 1, c_tile_rev & 1);
     if (grp < 0) return;  // a padding tile of the chunked grid (block-uniform, before any barrier)
     const int first = grp * G;
     const int ntl = TLOOP ? a0.tr.n : 1;
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = (L + C - 1) / C;
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, c_tile_rev & 4) * G;
     if (tr) {
         a.del_h += tr * a.tr.node;
         a.adf_h += tr * a.tr.edge;
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
     int j, u, tr;
     slot_of(threadIdx.x, L / C, invS, j, u);
     const int z0 = C * u;
-    const int k = group_tracer(trs.n, tr, c_tracer_major & 2) * G + j;
+    const int k = group_tracer(trs.n, tr, c_tracer_major & 2, c_tile_rev & 2) * G + j;
     plus += tr * trs.node;
     minus += tr * trs.node;
     adf_h += tr * trs.edge;
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
     __shared__ int4 s_ei[kB3hPackEdges];
     __shared__ int s_off[kB3hPackEdges + 1];
     int tr;
-    const int g = group_tracer(trs.n, tr, c_tracer_major & 2);
+    const int g = group_tracer(trs.n, tr, c_tracer_major & 2, c_tile_rev & 2);
     plus += tr * trs.node;
     minus += tr * trs.node;
     adf_h += tr * trs.edge;
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(1024) void k_b3h_u(const int4 *__restrict__ einfo, 
                                                 real *__restrict__ adf_h, Tracers trs)
 {
     int tr;
-    const int ug = group_tracer(trs.n, tr, c_tracer_major & 2);
+    const int ug = group_tracer(trs.n, tr, c_tracer_major & 2, c_tile_rev & 2);
     b3h_groups<C, U, NT, ODD>(einfo, n_edges, L, G, invS, plus + tr * trs.node, minus + tr * trs.node,
                               adf_h + tr * trs.edge, ug);
 }
@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
 {
     extern __shared__ real lds[];  // NodeRec[G]
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, c_tile_rev & 4) * G;
     if (tr) {
         a.plus += tr * a.tr.node;
         a.minus += tr * a.tr.node;
@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(1024) void k_b3h_iter(const int4 *__restrict__ einf
     int j, u, tr;
     slot_of(threadIdx.x, L / C, invS, j, u);
     const int z0 = C * u;
-    const int k = group_tracer(trs.n, tr, c_tracer_major & 2) * G + j;
+    const int k = group_tracer(trs.n, tr, c_tracer_major & 2, c_tile_rev & 2) * G + j;
     if (j >= G || k >= n_edges) return;
     plus += tr * trs.node;
     minus += tr * trs.node;
