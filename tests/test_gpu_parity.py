@@ -720,3 +720,32 @@ def test_kernel_timing_only_times_the_named_kernel():
     want = O.full_pass(m, f)
     for k, g in got.items():
         assert np.array_equal(g, want[k]), k
+
+
+@pytest.mark.parametrize("path", ["split", "fused", "stepwise"])
+def test_mesh_without_edges_matches_oracle(path):
+    """The edge loops' empty case (myDim_edge2D = 0, a partition with no local edges): b1h, b3h and
+    c-horizontal are no-ops, every launch over the edges has zero blocks, and the rest of the pass
+    equals the oracle's (which the reference's loops admit, tests/test_oracle.py)."""
+    import dataclasses
+    m0, f0 = mesh("tiny")
+    m = dataclasses.replace(m0, E=0)
+    f = dict(f0, adf_h=np.zeros(0))
+    want = O.full_pass(m, f)
+    abi.set_path("fused" if path == "split" else path)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        st = e.split_pass() if path == "split" else e.full_pass(fused=path == "fused")
+        e.sync()
+        assert st == 9, abi.last_error()
+        got = {k: e.download(k) for k in ("plus", "minus", "adf_v", "del_v", "del_h")}
+    finally:
+        e.free()
+        dm.free()
+        abi.set_path("fused")
+    L = m.L
+    for k in ("plus", "minus"):
+        assert_cols_equal(got[k], want[k], m.nlev_nod, L, m.N, k)
+    for k in ("adf_v", "del_v", "del_h"):
+        assert np.array_equal(got[k][: want[k].size], want[k]), k
