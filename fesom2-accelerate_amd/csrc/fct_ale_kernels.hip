@@ -319,9 +319,13 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // reference entry sequence's fct_ale_pre_comm_acc_ in the fast mode: it has no del_ttf_advvert,
 // hnode, hnode_new or area; fct_ale_c_acc_ does cv).
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
-__device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G, float invS)
+__device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G, float invS, int grp_in = -1,
+                                        const NodeRec *recs_in = nullptr)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
+    // OPT & 256: a persistent block's tile (k_p1p): the column group and its records (already in LDS,
+    // prefetched by DMA during the previous tile) come from the caller
+    constexpr bool PERSIST = (OPT & 256) != 0;
     // OPT & 128 (VERT): the block runs its G columns for every tracer of the batch in turn -- the
     // records, the internal-edge entries and the slot geometry are set up once, and the shared mesh
     // fields (area_inv, area, hnode, hnode_new) of the block's columns come back from L2 for the
@@ -329,9 +333,13 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     constexpr bool TLOOP = (OPT & 128) != 0;
     static_assert(!TLOOP || VERT, "the tracer loop keeps every thread in every barrier: VERT forms only");
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+    // persistent: an opaque copy per tile, so nothing derived from the thread index is hoisted out of
+    // the caller's tile loop and kept live across it (registers = occupancy)
+    if constexpr (PERSIST) asm volatile("" : "+v"(t));
     int tr0 = 0;
-    const int grp = TLOOP ? block_tile()
+    const int grp = PERSIST ? grp_in
+                    : TLOOP ? block_tile()
                     : a0.tr.chunk > 0 ? group_tracer_chunked(a0.tr.n, (a0.n_owned + G - 1) / G, a0.tr.chunk, tr0)
                                       : group_tracer(a0.tr.n, tr0, c_tracer_major & 1, c_tile_rev & 1);
     if (grp < 0) return;  // a padding tile of the chunked grid (block-uniform, before any barrier)
@@ -374,7 +382,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     // (behind the records and the internal-edge staging: p1_lds_bytes)
     real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
-    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
+    const NodeRec *recs = PERSIST ? recs_in : stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
         if (t < int_n)  // wave 0 (int_n <= kMaxInternal = kWave): lane t's entry lands at ie_ent[t]
             __builtin_amdgcn_global_load_lds(
@@ -707,6 +715,80 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
 {
     p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
+
+#if F2A_TUNING
+// Persistent p1v (tuning build, FESOM2_P1V_PERSIST=1): a grid of resident blocks, block k of XCD x
+// (blocks are dealt to the XCDs round-robin) runs the column groups start_x + k, + B, + 2B, ... of
+// its XCD's contiguous range (B blocks per XCD), so the XCDs sweep their ranges as with one block per
+// group.  While a tile runs, the next tile's NodeRecs go global -> LDS by DMA into the other record
+// buffer (landed by the tile's first barrier): the dependent records round trip at the head of every
+// block's chain is hidden.  One tracer, vlimit 1, level pairs.  The arguments are re-read from the
+// kernarg segment every tile (an opaque pointer), so the compiler cannot keep the ~60 argument words
+// live across the tile loop (SGPR spills into VGPRs would cost the occupancy the body needs).
+struct P1PArgs {
+    MeshPlanDev mp;
+    P1Args a;
+    int G, rec1_off;
+    float invS;
+};
+
+template <int OPT, bool ODD>
+__device__ __forceinline__ void p1p_body()
+{
+    extern __shared__ real lds[];
+    typedef const __attribute__((address_space(4))) P1PArgs *KArgs;
+    KArgs ka = (KArgs)(__builtin_amdgcn_kernarg_segment_ptr());
+    const int G = ka->G, L = ka->a.nl - 1, n_owned = ka->a.n_owned;
+    const int groups = (n_owned + G - 1) / G;
+    const int q = groups >> 3, r = groups & 7, x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int start = x * q + (x < r ? x : r), len = q + (x < r ? 1 : 0);
+    const int B = (int)(gridDim.x >> 3);
+    if (k >= len) return;  // block-uniform, before any barrier
+    constexpr int kChunks = sizeof(NodeRec) / 16;
+    {  // the first tile's records: plain loads + barrier
+        const int first = (start + k) * G, ncol = min(G, n_owned - first);
+        stage_records(ka->mp.node_rec, first, ncol, lds + 2 * G * L);
+    }
+    // loop state in SGPRs only (readfirstlane): every VGPR the loop carried would cost the body
+    // occupancy
+#pragma clang loop unroll(disable)
+    for (int i = 0;; i++) {
+        const int j = __builtin_amdgcn_readfirstlane(k + i * B);
+        KArgs kt = ka;
+        asm volatile("" : "+s"(kt));  // re-read the arguments for this tile
+        MeshPlanDev mp;
+        __builtin_memcpy(&mp, (const MeshPlanDev *)&kt->mp, sizeof mp);
+        P1Args a;
+        __builtin_memcpy(&a, (const P1Args *)&kt->a, sizeof a);
+        const int g = start + j;
+        const bool more = j + B < len;
+        const int cur = __builtin_amdgcn_readfirstlane((i & 1) ? kt->rec1_off : 2 * G * L);
+        const int nxt = __builtin_amdgcn_readfirstlane((i & 1) ? 2 * G * L : kt->rec1_off);
+        if (more) {  // next tile's records into the other buffer (wave w: bytes [1024 w, 1024 w + 1024))
+            const int first_n = (g + B) * G, ncol_n = min(G, n_owned - first_n);
+            const int w = (int)(threadIdx.x >> 6), idx = (int)threadIdx.x;
+            if (idx < ncol_n * kChunks)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(reinterpret_cast<const char *>(mp.node_rec + first_n) + 16 * idx),
+                    (__attribute__((address_space(3))) void *)(reinterpret_cast<char *>(lds + nxt) + 1024 * w), 16, 0, 0);
+        }
+        p1_body<1, 2, 2, 2, true, true, OPT | 256, ODD>(mp, a, G, kt->invS, g, reinterpret_cast<const NodeRec *>(lds + cur));
+        if (!more) break;
+        __syncthreads();  // the tile's LDS reads are done before the next one writes
+    }
+}
+template <int OPT, bool ODD>
+__global__ __launch_bounds__(1024) void k_p1p(P1PArgs)
+{
+    p1p_body<OPT, ODD>();
+}
+// held to 8 waves/SIMD (6 blocks per CU as the product p1v; the tile loop's extra registers spill)
+template <int OPT, bool ODD>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_p1p8(P1PArgs)
+{
+    p1p_body<OPT, ODD>();
+}
+#endif
 
 // p1 held to W waves/SIMD (amdgpu_waves_per_eu): the register allocator trades a few spills for
 // occupancy where a form sits just above a VGPR step (65 VGPRs = 7 waves, 74 = 6)
@@ -1534,6 +1616,43 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, b, G, inv);
             if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, b, G, inv);
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, b, G, inv);
+        }
+    }
+    // FESOM2_P1V_PERSIST = 1: persistent blocks with the next tile's records prefetched (k_p1p)
+    if (knob("FESOM2_P1V_PERSIST", 0) && a.vlimit == 1 && a.tr.n == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = group_columns(S);
+            const long groups = (long)(a.n_owned + G - 1) / G;
+            const size_t lds0 = p1_lds_bytes(G, L, 1, in);
+            const int rec1_off = (int)((lds0 + 15) / 16 * 16 / sizeof(real));
+            const size_t lds = rec1_off * sizeof(real) + (size_t)G * sizeof(NodeRec);
+            const unsigned threads = threads_for(G, S);
+            auto launch = [&](const void *fn, auto kern) -> hipError_t {
+                int per_cu = 0, dev = 0;
+                hipDeviceProp_t prop;
+                if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)threads, lds) != hipSuccess || per_cu < 1)
+                    return hipErrorInvalidValue;
+                long grid = (long)per_cu * prop.multiProcessorCount / 8 * 8;
+                grid = std::min(grid, (groups + 7) / 8 * 8);
+                if (grid < 8) grid = 8;
+                init_swizzle();
+                P1PArgs pa{mp, a, G, rec1_off, 1.0f / (float)S};
+                hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), lds, s, pa);
+                return hipGetLastError();
+            };
+            if (knob("FESOM2_P1V_PERSIST", 0) == 2) {
+                if (odd && in) return launch((const void *)k_p1p8<52, true>, k_p1p8<52, true>);
+                if (odd) return launch((const void *)k_p1p8<4, true>, k_p1p8<4, true>);
+                if (in) return launch((const void *)k_p1p8<52, false>, k_p1p8<52, false>);
+                return launch((const void *)k_p1p8<4, false>, k_p1p8<4, false>);
+            }
+            if (odd && in) return launch((const void *)k_p1p<52, true>, k_p1p<52, true>);
+            if (odd) return launch((const void *)k_p1p<4, true>, k_p1p<4, true>);
+            if (in) return launch((const void *)k_p1p<52, false>, k_p1p<52, false>);
+            return launch((const void *)k_p1p<4, false>, k_p1p<4, false>);
         }
     }
     // FESOM2_P1V_BATCH = 10*RB + EB: the production forms with other gather batches (cluster nodes /
