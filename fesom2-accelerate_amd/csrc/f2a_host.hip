@@ -192,7 +192,7 @@ struct TimedLaunch {
     std::string name;
     hipEvent_t start = nullptr, stop = nullptr;
 };
-bool g_timing = false;
+std::atomic<bool> g_timing{false};  // read per launch without the mutex
 std::string g_timing_only;  // fesom2_kernel_timing_only_: time only launches of this name (empty: all)
 std::mutex g_tmutex;
 std::vector<TimedLaunch *> g_pending;
