@@ -29,7 +29,11 @@ static __constant__ int c_ablate = 0;
 static __constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
 // FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range backwards, so it
 // starts on the data the previous kernel touched last (still in the Infinity Cache)
+#if F2A_TUNING
 static __constant__ int c_tile_rev = 0;
+#else
+static constexpr int c_tile_rev = 0;  // the product walks every range forwards
+#endif
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
 {
