@@ -266,55 +266,36 @@ __device__ __forceinline__ void stv_s(real *__restrict__ p, const real (&v)[C], 
 }
 
 // Odd L in pairs (C = 2, S = (L+1)/2 slots per column): the last slot of a column holds the one
-// level z0 = L-1 (`last1`).  Its pair load starts one level earlier, inside the column, and keeps the
-// upper value, so no load reaches into the next column or past the end of an array.
+// level z0 = L-1 (`last1`).  Its pair load reads that level and the next one -- the next column's
+// first level, or for the last column of an array the allocation's pad (kAllocPad) -- and the
+// second value is never used: every consumer guards the levels beyond the column (stores write
+// `nw` levels, gathers test z0 + c < lev, the LDS images skip it).  Round 2 shifted the last pair
+// one level back instead (`p - 1`, then a select per value): the selects and the shifted addresses
+// cost 8-10 VGPRs, i.e. 6-7 instead of 8 waves/SIMD for the odd-L p1v.  `last1` stays in the
+// signatures for the callers' guards.
 template <int C, bool ODD>
 __device__ __forceinline__ void ldo(const real *__restrict__ p, real (&v)[C], bool last1)
 {
-    if constexpr (ODD && C == 2) {
-        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(last1 ? p - 1 : p);
-        v[0] = last1 ? t.y : t.x;
-        v[1] = last1 ? 0. : t.y;
-    } else {
-        ldv<C>(p, v);
-    }
+    (void)last1;
+    ldv<C>(p, v);
 }
-// The same with the pointer already moved one level back for the last slot (p = column + z0 - last1):
-// no per-load address select
 template <int C, bool ODD>
 __device__ __forceinline__ void ldo_pre(const real *__restrict__ p, real (&v)[C], bool last1)
 {
-    if constexpr (ODD && C == 2) {
-        const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(p);
-        v[0] = last1 ? t.y : t.x;
-        v[1] = last1 ? 0. : t.y;
-    } else {
-        ldv<C>(p, v);
-    }
+    (void)last1;
+    ldv<C>(p, v);
 }
 template <int C, bool NT, bool ODD>
 __device__ __forceinline__ void ldo_s_pre(const real *__restrict__ p, real (&v)[C], bool last1)
 {
-    if constexpr (ODD && C == 2) {
-        const f2a_d2u *q = reinterpret_cast<const f2a_d2u *>(p);
-        const f2a_d2u t = NT ? __builtin_nontemporal_load(q) : *q;
-        v[0] = last1 ? t.y : t.x;
-        v[1] = last1 ? 0. : t.y;
-    } else {
-        ldv_s<C, NT>(p, v);
-    }
+    (void)last1;
+    ldv_s<C, NT>(p, v);
 }
 template <int C, bool NT, bool ODD>
 __device__ __forceinline__ void ldo_s(const real *__restrict__ p, real (&v)[C], bool last1)
 {
-    if constexpr (ODD && C == 2) {
-        const f2a_d2u *q = reinterpret_cast<const f2a_d2u *>(last1 ? p - 1 : p);
-        const f2a_d2u t = NT ? __builtin_nontemporal_load(q) : *q;
-        v[0] = last1 ? t.y : t.x;
-        v[1] = last1 ? 0. : t.y;
-    } else {
-        ldv_s<C, NT>(p, v);
-    }
+    (void)last1;
+    ldv_s<C, NT>(p, v);
 }
 
 // Columns of the stride-nl arrays (fct_adf_v, area, area_inv) start at 8-byte alignment only; a
@@ -357,7 +338,7 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
                                               const real *__restrict__ ttf, int z0, int L,
                                               real (&vx)[C], real (&vn)[C], bool last1 = false)
 {
-    const int zl = (ODD && C == 2 && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
+    const int zl = z0;  // odd L: the last pair reads one level past the column (ldo)
     for (int r = r0; r < r1; r += kBatch) {
         size_t idx[kBatch];
         int lev[kBatch];
@@ -404,7 +385,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
                                           const real *__restrict__ adf_h, int z0, int L, F &&f,
                                           bool last1 = false)
 {
-    const int zl = (ODD && C == 2 && last1) ? z0 - 1 : z0;  // pair load start (odd L: inside the column)
+    const int zl = z0;  // odd L: the last pair reads one level past the column (ldo)
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
         size_t idx[kBatch];
         int code[kBatch];

@@ -115,7 +115,10 @@ Buffer *allocate(void *host, size_t bytes, bool create_event)
     m->serial = track_object(m);
     m->host_pointer = host;
     m->size = bytes;
-    if (!ok(hipMalloc(&m->device_pointer, bytes ? bytes : 8), "hipMalloc")) {
+    // kAllocPad bytes of slack behind every array: the level-pair loads of odd-L columns read the
+    // level after a column's last one (the next column's first, discarded), and for the last column
+    // of an array that is the pad
+    if (!ok(hipMalloc(&m->device_pointer, bytes + kAllocPad), "hipMalloc")) {
         untrack_object(m);
         delete m;
         return nullptr;

@@ -32,6 +32,11 @@ static inline int knob(const char *name, int dflt)
 
 using real = double;
 
+// Slack behind every device array the library allocates (Buffer): kernels read odd-L columns in
+// 16-byte level pairs without shifting the last pair, so the last column of an array reads 8 bytes
+// past its end (see ldo in f2a_device.hpp).
+constexpr size_t kAllocPad = 64;
+
 // Buffer handle returned through void** (replaces the reference's struct gpuMemory,
 // include/fesom2-accelerate.h:19-28).  `magic` lets every entry point reject a stale or foreign
 // handle loudly instead of dereferencing it.

@@ -470,7 +470,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
-        const size_t bl = b - ((ODD && C == 2 && last1) ? 1 : 0);  // odd L: the last slot's pair starts a level early
+        const size_t bl = b;  // (odd L: the last slot's pair reads one level past the column, ldo)
         ldo_pre<C, ODD>(a.LO + bl, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
         ldo_pre<C, ODD>(a.ttf + bl, tt, last1);
         if constexpr (OPT & 1) {
@@ -679,7 +679,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                     hnn[c] = me[2 * gl_n + c];
                 }
             } else {
-                const size_t bl = b - ((ODD && C == 2 && last1) ? 1 : 0);
+                const size_t bl = b;
                 ldo_s_pre<C, NT, ODD>(a.del_v + bl, del_v, last1);
                 ldo_s_pre<C, NT, ODD>(a.hnode + bl, hn, last1);
                 ldo_s_pre<C, NT, ODD>(a.hnode_new + bl, hnn, last1);

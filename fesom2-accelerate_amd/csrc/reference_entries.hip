@@ -26,7 +26,7 @@ struct Staged {
     T *put(const T *host, size_t n)
     {
         void *p = nullptr;
-        if (!ok(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)), "hipMalloc(staging)")) return nullptr;
+        if (!ok(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T) + kAllocPad), "hipMalloc(staging)")) return nullptr;  // + pad: ldo
         ptrs.push_back(p);
         if (host && n && !ok(hipMemcpy(p, host, n * sizeof(T), hipMemcpyHostToDevice), "H2D(staging)")) return nullptr;
         return static_cast<T *>(p);
