@@ -1842,6 +1842,7 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
 #if F2A_TUNING
     const int KB = knob("FESOM2_P2_BATCH", 4);
     const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
+    if (C == 2 && NT && KB == 2) F2A_LAUNCH_GROUPS((k_p2<2, 2, true>), groups, G, S, lds, s, mp, a, G, invS);
     if (!NT || KB != 4) {
         if (C == 2 && KB == 8) F2A_LAUNCH_GROUPS((k_p2<2, 8, false>), groups, G, S, lds, s, mp, a, G, invS);
         if (C == 2) F2A_LAUNCH_GROUPS((k_p2<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1877,6 +1878,13 @@ hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const long groups = (a.count + G - 1) / G;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
+#if F2A_TUNING
+    // FESOM2_C_BATCH = 2: edge gathers in batches of 2 (fewer VGPRs, more resident waves)
+    if (knob("FESOM2_C_BATCH", 4) == 2) {
+        if (odd) F2A_LAUNCH_GROUPS((k_c<2, 2, true>), groups, G, S, lds, s, mp, a, G, invS);
+        F2A_LAUNCH_GROUPS((k_c<2, 2, false>), groups, G, S, lds, s, mp, a, G, invS);
+    }
+#endif
     if (odd) F2A_LAUNCH_GROUPS((k_c<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
     F2A_LAUNCH_GROUPS((k_c<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);
 }
