@@ -323,11 +323,12 @@ def main():
                     help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
-    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference"],
+    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference", "reference-plain"],
                     help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
                          "stepwise: one kernel per reference step; reference: the reference's entry sequence "
                          "pre_comm -> inter_comm -> post_comm -> c in its fast mode (fesom2_set_path_(2): b3v "
-                         "and the block-internal edges inside pre_comm)")
+                         "and the block-internal edges inside pre_comm); reference-plain: the same sequence without "
+                         "the fast mode (what a host that never calls fesom2_set_path_ gets)")
     ap.add_argument("--tracers", type=int, default=1,
                     help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
     ap.add_argument("--graph", action="store_true",
@@ -402,7 +403,7 @@ def main():
 
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
-    if args.tracers > 1 and args.path in ("stepwise", "reference"):
+    if args.tracers > 1 and args.path in ("stepwise", "reference", "reference-plain"):
         raise SystemExit("--tracers > 1 runs the batched (fused or split) entry points only")
     fields = synth.make_tracer_fields(m, args.tracers)
     f = fields[0]
@@ -499,7 +500,7 @@ def main():
         if world > 1 and args.exchange == "host":
             host_exchange()
             s2 = e.post_comm_c() if args.path == "fused" else (e.inter_comm(), e.post_comm(), e.c_step())[-1]
-        elif args.path in ("stepwise", "reference"):
+        elif args.path in ("stepwise", "reference", "reference-plain"):
             if halo is not None:
                 e.exchange(halo.comm, halo.plan)
             s2 = (e.inter_comm(), e.post_comm(), e.c_step())[-1]
