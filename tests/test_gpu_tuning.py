@@ -71,7 +71,13 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_P1V_B3H": "1", "FESOM2_CPT": "1"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3H_PACK": "0"},
                {"FESOM2_NT": "2"}, {"FESOM2_NT": "2", "FESOM2_P1V_B3H": "1"}, {"FESOM2_NT": "6", "FESOM2_P1V_B3H": "0"},
                {"FESOM2_BLOB": "1"}, {"FESOM2_BLOB": "1", "FESOM2_PATCH_ORDER": "1"}, {"FESOM2_BLOB": "0"},
-               {"FESOM2_P1V_B3H": "1", "FESOM2_P1V_INT_DMA": "0"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3HP_REG": "0"}]
+               {"FESOM2_P1V_B3H": "1", "FESOM2_P1V_INT_DMA": "0"}, {"FESOM2_P1V_B3H": "1", "FESOM2_B3HP_REG": "0"},
+               # round 3
+               {"FESOM2_P1V_BATCH": "23"}, {"FESOM2_P1V_BATCH": "32"}, {"FESOM2_P1V_BATCH": "33", "FESOM2_P1V_B3H": "1"},
+               {"FESOM2_P1V_BATCH": "62"}, {"FESOM2_P1V_BATCH": "26", "FESOM2_P1V_B3H": "1"},
+               {"FESOM2_P1V_PERSIST": "1"}, {"FESOM2_P1V_PERSIST": "1", "FESOM2_P1V_B3H": "1"},
+               {"FESOM2_P1V_PERSIST": "2", "FESOM2_P1V_B3H": "1"}, {"FESOM2_TILE_REV": "7"},
+               {"FESOM2_TILE_REV": "6", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_WAVES": "8"}]
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
@@ -107,3 +113,38 @@ def test_p2h_fuse_level_counts_and_repeats(nl, full, monkeypatch):
     finally:
         e.free()
         dm.free()
+
+
+@pytest.mark.parametrize("knobs", [{"FESOM2_C_BATCH": "2"}, {"FESOM2_P2_BATCH": "2"}],
+                         ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_reference_sequence_variants_match_oracle(knobs, name, monkeypatch):
+    """Round-3 node-kernel batches: the reference sequence's c-step (k_c) and the fused phase 2."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    m, f = mesh(name)
+    for fused in (True, False):
+        st, got = run_pass(m, f, fused=fused)
+        assert st == 9
+        check_pass(m, got, O.full_pass(m, f))
+
+
+@pytest.mark.parametrize("chunk", ["1", "3", "256"])
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_tracer_chunks_match_oracle(chunk, name, monkeypatch):
+    """FESOM2_TRACER_CHUNK: batched p1v in XCD-chunked tracer tiles (padding tiles past the last group
+    exit before any barrier); every tracer equals its own oracle pass."""
+    monkeypatch.setenv("FESOM2_TRACER_CHUNK", chunk)
+    m, _ = mesh(name)
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.split_pass() == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k).reshape(3, -1) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        e.free()
+        dm.free()
+    for t in range(3):
+        check_pass(m, {k: v[t] for k, v in got.items()}, O.full_pass(m, tracers[t]))
