@@ -19,6 +19,10 @@
 ! mode 3: mode 0's unmodified sequence and transfer semantics in the fast mode: fesom2_set_path_(2)
 !         and fesom2_bind_c_vertical_ once before the step (b3v, cv and the block-internal edges
 !         inside pre_comm, c-horizontal alone in the c-step)
+! Modes 1 and 2 take several tracers at once (FESOM2's tracer loop as one batched call, BASELINE
+! config 3): ttf, fct_LO, fct_adf_v, fct_adf_h, del_ttf_advvert and del_ttf_advhoriz then hold
+! ntracers Fortran arrays one after another, (nl-1, nod, ntracers) etc.; ntracers = size(ttf) /
+! ((myDim+eDim)*(nl-1)).  The mesh fields (area, area_inv, hnode, hnode_new) are shared.
 ! OUT: int32(4) alg_states, then fct_plus, fct_minus, fct_adf_v, fct_adf_h, del_ttf_advvert,
 !      del_ttf_advhoriz in the IN format.
 program fct_ale_host
@@ -49,9 +53,15 @@ program fct_ale_host
   call read_ra(u, area); call read_ra(u, area_inv); call read_ra(u, hnode); call read_ra(u, hnode_new)
   call read_ra(u, del_v); call read_ra(u, del_h); call read_ra(u, sc)
   close(u)
-  allocate(plus(NT * L), minus(NT * L))
+  ntr = 1
+  if (NT * L > 0) ntr = int(size(ttf) / (NT * L), c_int)
+  if (ntr < 1 .or. size(ttf) /= ntr * NT * L .or. ((mode == 0 .or. mode == 3) .and. ntr /= 1)) then
+    print *, 'fct_ale_host: ttf holds ', size(ttf), ' values: not a whole number of tracers for mode ', mode
+    error stop 4
+  end if
+  allocate(plus(NT * L * ntr), minus(NT * L * ntr))
   plus = 0; minus = 0
-  yes = .true.; no = .false.; zero = 0; one = 1; two = 2; ntr = 1; st = -1
+  yes = .true.; no = .false.; zero = 0; one = 1; two = 2; st = -1
   nullh = c_null_ptr
 
   call set_mpi_rank(zero, one)
@@ -121,7 +131,7 @@ program fct_ale_host
   call write_ra(u, plus); call write_ra(u, minus); call write_ra(u, adf_v); call write_ra(u, adf_h)
   call write_ra(u, del_v); call write_ra(u, del_h)
   close(u)
-  print '(a, 4i3)', 'fct_ale_host: alg_state', st
+  print '(a, 4i3, a, i3)', 'fct_ale_host: alg_state', st, '  tracers', ntr
 
 contains
 

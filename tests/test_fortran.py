@@ -23,8 +23,9 @@ ABI_NAMES = ("set_mpi_rank_", "transfer_mesh_", "alloc_var_", "reserve_var_", "t
              "transfer_var_async_", "make_stream_", "await_stream_")
 
 
-def write_input(path, m, f, mode, vlimit=1, dt=1.0, eps=1e-16, big=1e3):
-    """The driver's input file: int64 element count, then the elements, per array."""
+def write_input(path, m, f, mode, vlimit=1, dt=1.0, eps=1e-16, big=1e3, tracers=None):
+    """The driver's input file: int64 element count, then the elements, per array.  ``tracers``: a
+    list of field dicts whose per-tracer arrays are written one after another (modes 1 and 2)."""
     with open(path, "wb") as fh:
         def put(a, typ):
             a = np.ascontiguousarray(a, dtype=typ).reshape(-1)
@@ -33,8 +34,9 @@ def write_input(path, m, f, mode, vlimit=1, dt=1.0, eps=1e-16, big=1e3):
         put([m.N, m.H, m.T, m.E, m.nl, m.dim, vlimit, mode], np.int32)
         for k in ("nlev_nod", "nlev_elem", "elem2D_nodes", "nie_num", "nie", "edges", "edge_tri"):
             put(getattr(m, k), np.int32)
+        per_tracer = ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")
         for k in ("ttf", "LO", "adf_v", "adf_h", "area", "area_inv", "hnode", "hnode_new", "del_v", "del_h"):
-            put(f[k], np.float64)
+            put(np.concatenate([t[k] for t in tracers]) if tracers and k in per_tracer else f[k], np.float64)
         put([dt, eps, big], np.float64)
 
 
@@ -107,3 +109,30 @@ def test_fortran_host_matches_oracle(tmp_path, mode, name):
     assert_cols_equal(got["minus"], want["minus"], m.nlev_nod, m.L, m.N, "fct_minus")
     for k in ("adf_v", "adf_h", "del_v", "del_h"):
         assert np.array_equal(got[k], want[k]), k
+
+
+@pytest.mark.gpu
+@needs_flang
+@pytest.mark.parametrize("mode", [1, 2], ids=["resident_split", "graph_replay"])
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_fortran_host_batched_tracers(tmp_path, mode, name):
+    """FESOM2's tracer loop as one batched call from Fortran (BASELINE config 3's entry points):
+    3 tracers in (nl-1, nod, ntracers) arrays through fct_ale_pre_comm_v_acc_ / fct_ale_post_comm_h_acc_
+    with ntracers = 3, each tracer equal to its own oracle pass."""
+    import oracle as O
+    m = synth.config_mesh(name)
+    tracers = synth.make_tracer_fields(m, 3)
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    write_input(fin, m, tracers[0], mode, tracers=tracers)
+    r = subprocess.run([HOST, str(fin), str(fout)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tracers  3" in r.stdout, r.stdout
+    states, got = read_output(fout)
+    assert states == [7, 9, -1, -1], states
+    for t, f in enumerate(tracers):
+        want = O.full_pass(m, f)
+        part = {k: v.reshape(3, -1)[t] for k, v in got.items()}
+        assert_cols_equal(part["plus"], want["plus"], m.nlev_nod, m.L, m.N, f"tracer {t} fct_plus")
+        assert_cols_equal(part["minus"], want["minus"], m.nlev_nod, m.L, m.N, f"tracer {t} fct_minus")
+        for k in ("adf_v", "adf_h", "del_v", "del_h"):
+            assert np.array_equal(part[k], want[k]), (t, k)
