@@ -749,3 +749,27 @@ def test_mesh_without_edges_matches_oracle(path):
         assert_cols_equal(got[k], want[k], m.nlev_nod, L, m.N, k)
     for k in ("adf_v", "del_v", "del_h"):
         assert np.array_equal(got[k][: want[k].size], want[k]), k
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_shapes_split_and_batched(seed):
+    """Randomised shapes for the level-pair kernels (odd and even L from 2 to 63, shallow and full
+    depth, grids whose node count is no multiple of a block): the direction-split pass of one tracer
+    and a batch of two, each equal to the oracle.  Odd L exercises the pair loads that read one level
+    past a column (into the next column, or the allocation pad after the last one)."""
+    rng = np.random.default_rng(1000 + seed)
+    nx, ny, nl = int(rng.integers(5, 40)), int(rng.integers(4, 30)), int(rng.integers(3, 65))
+    m = synth.make_mesh(nx, ny, nl, seed=seed, full_depth=bool(seed % 2))
+    tracers = synth.make_tracer_fields(m, 2)
+    check_pass(m, run_split(m, tracers[0]), O.full_pass(m, tracers[0]))
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.split_pass() == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k).reshape(2, -1) for k in ("plus", "minus", "adf_v", "adf_h", "del_v", "del_h")}
+    finally:
+        e.free()
+        dm.free()
+    for t in range(2):
+        check_pass(m, {k: v[t] for k, v in got.items()}, O.full_pass(m, tracers[t]))
