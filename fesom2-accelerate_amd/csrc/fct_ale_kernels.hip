@@ -1481,9 +1481,8 @@ int p1v_group_columns(int nl)
 // columns per block of launch_p1v's shape for this vlimit (odd L in level pairs at vlimit 1 only)
 static int p1v_launch_G(int nl, int vlimit)
 {
-    const int L = nl - 1;
-    if (vlimit == 1) return p1v_group_columns(nl);
-    return group_columns(L / levels_per_thread(L));
+    (void)vlimit;  // every vlimit runs odd L in level pairs (round 3)
+    return p1v_group_columns(nl);
 }
 
 // the launch_p1v forms with the internal-edge tail: the plan built the lists for this block size
@@ -1529,6 +1528,18 @@ static bool launch_p1v_tloop(const MeshPlanDev &mp, const P1Args &a, hipStream_t
 static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in)
 {
     const int L = a.nl - 1;
+    if (odd_pairs(L) && a.vlimit != 1) {  // the product's forms (p1v_launch_G: pairs at every vlimit)
+        const int S = (L + 1) / 2, G = group_columns(S);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
+        const float inv = 1.0f / (float)S;
+        if (a.vlimit == 2) {
+            if (in) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+        if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+    }
     if (odd_pairs(L) && a.vlimit == 1) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
@@ -1708,13 +1719,22 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     // OPT 4: 16-byte loads/stores of the stride-nl arrays; +16 the block-internal edges'
     // b3-horizontal, +32 their entries staged into LDS by DMA.  NT: the single-use streams
     // (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
-    if (odd_pairs(L) && a.vlimit == 1) {
+    if (odd_pairs(L)) {  // odd L in level pairs, every vlimit (the 3-point bounds of vlimit 2/3 skip the pad level)
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-        const size_t lds = p1_lds_bytes(G, L, 1, in);
+        const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
-        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv);
-        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        switch (a.vlimit) {
+        case 2:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        case 3:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        default:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
+        }
     }
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
@@ -1758,13 +1778,22 @@ hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     if (launch_p1v_tloop<64>(mp, a, s, in, &err)) return err;
 #endif
     const int L = a.nl - 1;
-    if (odd_pairs(L) && a.vlimit == 1) {
+    if (odd_pairs(L)) {
         const int S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-        const size_t lds = p1_lds_bytes(G, L, 1, in);
+        const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
-        if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
-        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+        switch (a.vlimit) {
+        case 2:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+        case 3:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 20 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+        default:
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
+        }
     }
     const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;

@@ -545,10 +545,11 @@ def test_split_by_direction_matches_oracle(name, full, perm, resident, internal,
 
 
 @pytest.mark.parametrize("vlimit", [2, 3])
-@pytest.mark.parametrize("name,internal", [("8k x 20", "0"), ("8k x 20", "1"), ("127k x 47", "1")])
+@pytest.mark.parametrize("name,internal", [("8k x 20", "0"), ("8k x 20", "1"), ("127k x 47", "0"), ("127k x 47", "1")])
 def test_split_by_direction_vlimit(vlimit, name, internal, monkeypatch):
-    """vlimit 2/3 on the split path, with and without the block-internal edges limited in p1v (odd L:
-    the vlimit-2/3 shape has other blocks than the plan's lists, so p1v leaves them to b3h)."""
+    """vlimit 2/3 on the split path, with and without the block-internal edges limited in p1v (odd L
+    runs in level pairs at every vlimit since round 3, so the plan's internal-edge lists match the
+    vlimit-2/3 blocks too)."""
     monkeypatch.setenv("FESOM2_P1V_B3H", internal)
     m, f = mesh(name)
     st, p1 = O.pre_comm(m, f, vlimit=vlimit, vlimit_ext=True)
@@ -560,6 +561,8 @@ def test_split_by_direction_vlimit(vlimit, name, internal, monkeypatch):
         e.sync()
         for k in ("adf_v", "adf_h", "del_v", "del_h"):
             assert np.array_equal(e.download(k), want[k]), k
+        assert_cols_equal(e.download("plus"), p1["plus"], m.nlev_nod, m.L, m.N, "plus")
+        assert_cols_equal(e.download("minus"), p1["minus"], m.nlev_nod, m.L, m.N, "minus")
     finally:
         e.free()
         dm.free()
@@ -759,11 +762,12 @@ def test_random_shapes_split_and_batched(seed):
     past a column (into the next column, or the allocation pad after the last one)."""
     rng = np.random.default_rng(1000 + seed)
     nx, ny, nl = int(rng.integers(5, 40)), int(rng.integers(4, 30)), int(rng.integers(3, 65))
+    vl = 1 + seed % 3  # vlimit 1, 2, 3 in turn
     m = synth.make_mesh(nx, ny, nl, seed=seed, full_depth=bool(seed % 2))
     tracers = synth.make_tracer_fields(m, 2)
-    check_pass(m, run_split(m, tracers[0]), O.full_pass(m, tracers[0]))
+    check_pass(m, run_split(m, tracers[0], vlimit=vl), O.full_pass(m, tracers[0], vlimit=vl))
     dm = engine.DeviceMesh(m)
-    e = engine.FctAleBatch(dm, tracers)
+    e = engine.FctAleBatch(dm, tracers, vlimit=vl)
     try:
         assert e.split_pass() == 9, abi.last_error()
         e.sync()
@@ -772,4 +776,4 @@ def test_random_shapes_split_and_batched(seed):
         e.free()
         dm.free()
     for t in range(2):
-        check_pass(m, {k: v[t] for k, v in got.items()}, O.full_pass(m, tracers[t]))
+        check_pass(m, {k: v[t] for k, v in got.items()}, O.full_pass(m, tracers[t], vlimit=vl))
