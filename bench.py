@@ -18,7 +18,10 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
             (N = 8 is BASELINE configs[4]'s 9.6M-node mesh).
 * value     cell-updates/s = (sum over ranks of owned wet cells N_owned x L) / (max-over-ranks time per step).
 * roofline  the dominant kernel's algorithmic bytes per launch / its average launch time (HIP events
-            on its stream, recorded inside the library around every launch), against 8.0 TB/s.
+            on its stream, recorded inside the library around each of its launches in the timed region;
+            the other kernels are timed on up to 10 extra steps after it), against 8.0 TB/s.
+* check     one more pass on pristine inputs, compared cell for cell with the oracle (per rank on its
+            local mesh at N > 1); a mismatch exits with status 1.
 * cpu_baseline  the oracle's single-threaded full pass (bit-identical to reference.cpp for a1..b2)
             on the same mesh, rank 0 at N = 1 only; plus "all_cores": P single-threaded oracle
             processes on a P-way strip partition of the same mesh (MPI-style replicas, SURVEY.md
