@@ -370,6 +370,109 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
     }
 }
 
+// Memory-level parallelism beyond the register file (tuning build, FESOM2_P1V_DMA): per round trip
+// one more gathered column pair lands in LDS by DMA (global_load_lds_dwordx4: no destination VGPRs)
+// beside the kBatch register loads, so a trip covers kBatch + 1 cluster nodes / edges.  `slot` is
+// the wave's 1 KB region (lane i's 16 bytes at slot + 2 i doubles); the wave waits for all of its
+// loads (vmcnt(0)) before it reads its slots back.  C = 2 only.
+__device__ __forceinline__ void dma16(const real *src, real *slot_wave)
+{
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)slot_wave, 16, 0, 0);
+}
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int kBatch>
+__device__ __forceinline__ void cluster_bound_dma(const RingRef *__restrict__ ring, int r0, int r1,
+                                                  const real *__restrict__ LO, const real *__restrict__ ttf,
+                                                  int z0, int L, real (&vx)[2], real (&vn)[2], real *slo, real *stt,
+                                                  int lane)
+{
+    for (int r = r0; r < r1; r += kBatch + 1) {
+        const RingRef rd = (r < r1) ? ring[r] : RingRef{0, 0};
+        if (z0 < rd.lev) {
+            dma16(LO + (size_t)rd.node * L + z0, slo);
+            dma16(ttf + (size_t)rd.node * L + z0, stt);
+        }
+        size_t idx[kBatch];
+        int lev[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const RingRef rr = (r + 1 + k < r1) ? ring[r + 1 + k] : RingRef{0, 0};
+            idx[k] = (size_t)rr.node * L + z0;
+            lev[k] = rr.lev;
+        }
+        real lo[kBatch][2], tt[kBatch][2];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < lev[k]) {
+                ldv<2>(LO + idx[k], lo[k]);
+                ldv<2>(ttf + idx[k], tt[k]);
+            } else {
+                lo[k][0] = lo[k][1] = tt[k][0] = tt[k][1] = 0.;
+            }
+        }
+        wait_vm_all();
+        if (z0 < rd.lev) {
+            const real d0 = slo[2 * lane], d1 = slo[2 * lane + 1], e0 = stt[2 * lane], e1 = stt[2 * lane + 1];
+            vx[0] = RMAX(vx[0], RMAX(d0, e0));
+            vn[0] = RMIN(vn[0], RMIN(d0, e0));
+            if (z0 + 1 < rd.lev) {
+                vx[1] = RMAX(vx[1], RMAX(d1, e1));
+                vn[1] = RMIN(vn[1], RMIN(d1, e1));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+                if (z0 + c < lev[k]) {
+                    vx[c] = RMAX(vx[c], RMAX(lo[k][c], tt[k][c]));
+                    vn[c] = RMIN(vn[c], RMIN(lo[k][c], tt[k][c]));
+                }
+    }
+}
+
+// ascending edge order kept: the DMA'd edge is the first of each trip
+template <int kBatch, class F>
+__device__ __forceinline__ void for_edges_dma(const EdgeRef *__restrict__ edges, int e0, int e1,
+                                              const real *__restrict__ adf_h, int z0, int L, F &&f, real *sh,
+                                              int lane)
+{
+    for (int k0 = e0; k0 < e1; k0 += kBatch + 1) {
+        const EdgeRef ed = edges[k0];
+        const int dlev = ed.code >> 1;
+        if (z0 < dlev) dma16(adf_h + (size_t)ed.edge * L + z0, sh);
+        size_t idx[kBatch];
+        int code[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const EdgeRef er = (k0 + 1 + k < e1) ? edges[k0 + 1 + k] : EdgeRef{0, 0, 0};
+            idx[k] = (size_t)er.edge * L + z0;
+            code[k] = er.code;
+        }
+        real h[kBatch][2];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            if (z0 < (code[k] >> 1)) {
+                ldv<2>(adf_h + idx[k], h[k]);
+            } else {
+                h[k][0] = h[k][1] = 0.;
+            }
+        }
+        wait_vm_all();
+        if (z0 < dlev) {
+            f(0, sh[2 * lane], ed.code & 1);
+            if (z0 + 1 < dlev) f(1, sh[2 * lane + 1], ed.code & 1);
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+                if (z0 + c < (code[k] >> 1)) f(c, h[k][c], code[k] & 1);
+    }
+}
+
 // Gather the fct_adf_h levels z0..z0+C-1 of a node's edges (CSR slice [e0, e1), ascending edge
 // order) and hand each (value, second-endpoint flag) to `f(c, h, second)` in that order.
 // agent-coherent loads (read-only data another workgroup of this launch published: no L1 hit)

@@ -491,6 +491,17 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
             }
         const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
+        // OPT & 512 (tuning build, FESOM2_P1V_DMA): one more cluster node / edge per round trip by LDS
+        // DMA (dma_base: 3 KB per wave behind the kernel's other LDS)
+        real *dma_w = nullptr;
+        if constexpr ((OPT & 512) != 0) {
+            const size_t off = (reinterpret_cast<size_t>(cmx + (VLIMIT != 1 ? G * L : 0)) + 15) & ~size_t(15);
+            dma_w = reinterpret_cast<real *>(off) + (size_t)(threadIdx.x >> 6) * 384;
+        }
+        if constexpr ((OPT & 512) != 0 && C == 2)
+            cluster_bound_dma<RB>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, dma_w, dma_w + 128,
+                                  (int)(threadIdx.x & 63));
+        else
         cluster_bound<C, RB, ODD>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
         if (no > kRecRing)
             cluster_bound<C, RB, ODD>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn, last1);
@@ -511,6 +522,9 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 m[c] += RMIN(0., h);
             }
         };
+        if constexpr ((OPT & 512) != 0 && C == 2)
+            for_edges_dma<EB>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, dma_w + 256, (int)(threadIdx.x & 63));
+        else
         for_edges<C, EB, false, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
         if (ne > kRecEdge) for_edges<C, EB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     }
@@ -1664,6 +1678,28 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             if (odd) return launch((const void *)k_p1p<4, true>, k_p1p<4, true>);
             if (in) return launch((const void *)k_p1p<52, false>, k_p1p<52, false>);
             return launch((const void *)k_p1p<4, false>, k_p1p<4, false>);
+        }
+    }
+    // FESOM2_P1V_DMA = 1: one more cluster node and edge per gather round trip through LDS DMA
+    if (knob("FESOM2_P1V_DMA", 0) && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = group_columns(S);
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const unsigned threads = threads_for(G, S);
+            const size_t lds = (p1_lds_bytes(G, L, 1, in) + 15) / 16 * 16 + (size_t)(threads / 64) * 3072;
+            const float inv = 1.0f / (float)S;
+            if (knob("FESOM2_P1V_DMA", 0) == 2) {  // held to 8 waves/SIMD
+                if (odd && in) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+                if (odd) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 4 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+                if (in) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+                F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 4 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+            }
+            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
     // FESOM2_P1V_BATCH = 10*RB + EB: the production forms with other gather batches (cluster nodes /
