@@ -1874,6 +1874,8 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
         const float invS = 1.0f / (float)S;
 #if F2A_TUNING
         if (!NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (knob("FESOM2_P2H_BATCH", 4) == 6) F2A_LAUNCH_GROUPS((k_p2h<2, 6, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (knob("FESOM2_P2H_BATCH", 4) == 8) F2A_LAUNCH_GROUPS((k_p2h<2, 8, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
 #endif
         F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
@@ -1883,6 +1885,11 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const size_t lds = (size_t)G * sizeof(NodeRec);
 #if F2A_TUNING
     if (C == 2) {
+        // FESOM2_P2H_BATCH: edge gathers per round trip (6 or 8: a structured node's 6 edges in one)
+        if (NT && pair && knob("FESOM2_P2H_BATCH", 4) == 6)
+            F2A_LAUNCH_GROUPS((k_p2h<2, 6, true, true>), groups, G, S, lds, s, mp, a, G, invS);
+        if (NT && pair && knob("FESOM2_P2H_BATCH", 4) == 8)
+            F2A_LAUNCH_GROUPS((k_p2h<2, 8, true, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (NT && !pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (!NT && pair) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (!NT) F2A_LAUNCH_GROUPS((k_p2h<2, 4, false>), groups, G, S, lds, s, mp, a, G, invS);

@@ -78,7 +78,8 @@ SPLIT_KNOBS = [{"FESOM2_P1V_EARLY": "1"}, {"FESOM2_P1V_EARLY": "2"}, {"FESOM2_P1
                {"FESOM2_P1V_PERSIST": "1"}, {"FESOM2_P1V_PERSIST": "1", "FESOM2_P1V_B3H": "1"},
                {"FESOM2_P1V_PERSIST": "2", "FESOM2_P1V_B3H": "1"}, {"FESOM2_TILE_REV": "7"},
                {"FESOM2_TILE_REV": "6", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_WAVES": "8"},
-               {"FESOM2_P1V_DMA": "1"}, {"FESOM2_P1V_DMA": "2", "FESOM2_P1V_B3H": "1"}]
+               {"FESOM2_P1V_DMA": "1"}, {"FESOM2_P1V_DMA": "2", "FESOM2_P1V_B3H": "1"},
+               {"FESOM2_P2H_BATCH": "6"}, {"FESOM2_P2H_BATCH": "8"}]
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
