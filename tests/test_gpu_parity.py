@@ -777,3 +777,15 @@ def test_random_shapes_split_and_batched(seed):
         dm.free()
     for t in range(2):
         check_pass(m, {k: v[t] for k, v in got.items()}, O.full_pass(m, tracers[t], vlimit=vl))
+
+
+@pytest.mark.parametrize("nl,full", [(129, True), (129, False), (200, True), (200, False)])
+def test_deep_columns_split_pass(nl, full, monkeypatch):
+    """Deep columns (L = 128, 199): blocks of up to 832 threads, the LDS stencil and the internal-edge
+    tail at that depth, odd and even L; the split pass with and without block-internal edges."""
+    m = synth.make_mesh(24, 10, nl, seed=nl, full_depth=full)
+    f = synth.make_fields(m)
+    want = O.full_pass(m, f)
+    for internal in ("0", "1"):
+        monkeypatch.setenv("FESOM2_P1V_B3H", internal)  # a plan option: read when run_split builds the plan
+        check_pass(m, run_split(m, f), want)
