@@ -190,13 +190,15 @@ def test_batched_split_by_direction(internal, monkeypatch):
         dm.free()
 
 
+@pytest.mark.parametrize("nl", [21, 48])
 @pytest.mark.parametrize("internal", ["0", "1"])
-def test_split_by_direction_partitioned_overlap(comm, internal, monkeypatch):
+def test_split_by_direction_partitioned_overlap(comm, internal, nl, monkeypatch):
     """Two partitions, 2 tracers, the split entries with the exchange inside fct_ale_post_comm_h_acc_
     (deranged halo repaired only by the one-rank exchange, as test_batched_partitioned_exchange);
-    with and without the block-internal edges limited in p1v."""
+    with and without the block-internal edges limited in p1v; even and odd L (the interior and
+    boundary launches of b3h / c-horizontal in their level-pair forms)."""
     monkeypatch.setenv("FESOM2_P1V_B3H", internal)
-    nx, ny, nl, ntr = 64, 48, 21, 2
+    nx, ny, ntr = 64, 48, 2
     g = synth.make_mesh(nx, ny, nl)
     gtr = synth.make_tracer_fields(g, ntr)
     wants = [O.full_pass(g, t) for t in gtr]
