@@ -1,5 +1,5 @@
 // f2a_device.hpp -- device helpers and launch utilities shared by the kernel files
-// (fct_ale_kernels.hip: production kernels; fct_ale_variants.hip: measured alternatives).
+// (fct_ale_kernels.hip).
 //
 // Each kernel file is its own device code object, so the __constant__ switches are per file
 // (static) and every file's launchers initialise their own copy (init_swizzle).
@@ -22,8 +22,7 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 // residue class a contiguous range of tiles.  Speed only, never correctness.
 static __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements, tuning build)
 // FESOM2_ABLATE (tuning build, timing-only experiments, results are wrong): bit 0 skips the cluster
-// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2, bit 3 the arrival
-// counters of the fused b3h.
+// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2.
 static __constant__ int c_ablate = 0;
 // FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile order
 static __constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
@@ -143,23 +142,6 @@ __device__ __forceinline__ void slot_of(int t, int S, float invS, int &j, int &u
 }
 
 __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDim.x); }
-
-// XCD-chunked tracer tiles: XCD x (blocks b with b % 8 == x, dispatched round-robin) owns column
-// groups [x*gx, (x+1)*gx), gx = ceil(groups/8), and walks them in chunks of K groups, each chunk
-// once per tracer -- the tracers' passes over a chunk follow each other, so each keeps the
-// single-tracer reuse distance of the neighbour gathers, and the chunk's records and mesh fields
-// come back from L2 / the Infinity Cache for the later tracers.  Grid: 8 * gx * ntr blocks;
-// returns -1 for the padding tiles past the last group.
-__device__ __forceinline__ int group_tracer_chunked(int ntr, int groups, int K, int &tr)
-{
-    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-    const int gx = (groups + 7) >> 3, span = K * ntr;
-    const int c = k / span, r = k - c * span;
-    const int kc = min(K, gx - c * K);
-    tr = r / kc;
-    const int g = x * gx + c * K + (r - tr * kc);
-    return g < groups ? g : -1;
-}
 
 // tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
 // for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
@@ -370,120 +352,9 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
     }
 }
 
-// Memory-level parallelism beyond the register file (tuning build, FESOM2_P1V_DMA): per round trip
-// one more gathered column pair lands in LDS by DMA (global_load_lds_dwordx4: no destination VGPRs)
-// beside the kBatch register loads, so a trip covers kBatch + 1 cluster nodes / edges.  `slot` is
-// the wave's 1 KB region (lane i's 16 bytes at slot + 2 i doubles); the wave waits for all of its
-// loads (vmcnt(0)) before it reads its slots back.  C = 2 only.
-__device__ __forceinline__ void dma16(const real *src, real *slot_wave)
-{
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                     (__attribute__((address_space(3))) void *)slot_wave, 16, 0, 0);
-}
-__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-template <int kBatch>
-__device__ __forceinline__ void cluster_bound_dma(const RingRef *__restrict__ ring, int r0, int r1,
-                                                  const real *__restrict__ LO, const real *__restrict__ ttf,
-                                                  int z0, int L, real (&vx)[2], real (&vn)[2], real *slo, real *stt,
-                                                  int lane)
-{
-    for (int r = r0; r < r1; r += kBatch + 1) {
-        const RingRef rd = (r < r1) ? ring[r] : RingRef{0, 0};
-        if (z0 < rd.lev) {
-            dma16(LO + (size_t)rd.node * L + z0, slo);
-            dma16(ttf + (size_t)rd.node * L + z0, stt);
-        }
-        size_t idx[kBatch];
-        int lev[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            const RingRef rr = (r + 1 + k < r1) ? ring[r + 1 + k] : RingRef{0, 0};
-            idx[k] = (size_t)rr.node * L + z0;
-            lev[k] = rr.lev;
-        }
-        real lo[kBatch][2], tt[kBatch][2];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            if (z0 < lev[k]) {
-                ldv<2>(LO + idx[k], lo[k]);
-                ldv<2>(ttf + idx[k], tt[k]);
-            } else {
-                lo[k][0] = lo[k][1] = tt[k][0] = tt[k][1] = 0.;
-            }
-        }
-        wait_vm_all();
-        if (z0 < rd.lev) {
-            const real d0 = slo[2 * lane], d1 = slo[2 * lane + 1], e0 = stt[2 * lane], e1 = stt[2 * lane + 1];
-            vx[0] = RMAX(vx[0], RMAX(d0, e0));
-            vn[0] = RMIN(vn[0], RMIN(d0, e0));
-            if (z0 + 1 < rd.lev) {
-                vx[1] = RMAX(vx[1], RMAX(d1, e1));
-                vn[1] = RMIN(vn[1], RMIN(d1, e1));
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; k++)
-#pragma unroll
-            for (int c = 0; c < 2; c++)
-                if (z0 + c < lev[k]) {
-                    vx[c] = RMAX(vx[c], RMAX(lo[k][c], tt[k][c]));
-                    vn[c] = RMIN(vn[c], RMIN(lo[k][c], tt[k][c]));
-                }
-    }
-}
-
-// ascending edge order kept: the DMA'd edge is the first of each trip
-template <int kBatch, class F>
-__device__ __forceinline__ void for_edges_dma(const EdgeRef *__restrict__ edges, int e0, int e1,
-                                              const real *__restrict__ adf_h, int z0, int L, F &&f, real *sh,
-                                              int lane)
-{
-    for (int k0 = e0; k0 < e1; k0 += kBatch + 1) {
-        const EdgeRef ed = edges[k0];
-        const int dlev = ed.code >> 1;
-        if (z0 < dlev) dma16(adf_h + (size_t)ed.edge * L + z0, sh);
-        size_t idx[kBatch];
-        int code[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            const EdgeRef er = (k0 + 1 + k < e1) ? edges[k0 + 1 + k] : EdgeRef{0, 0, 0};
-            idx[k] = (size_t)er.edge * L + z0;
-            code[k] = er.code;
-        }
-        real h[kBatch][2];
-#pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            if (z0 < (code[k] >> 1)) {
-                ldv<2>(adf_h + idx[k], h[k]);
-            } else {
-                h[k][0] = h[k][1] = 0.;
-            }
-        }
-        wait_vm_all();
-        if (z0 < dlev) {
-            f(0, sh[2 * lane], ed.code & 1);
-            if (z0 + 1 < dlev) f(1, sh[2 * lane + 1], ed.code & 1);
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; k++)
-#pragma unroll
-            for (int c = 0; c < 2; c++)
-                if (z0 + c < (code[k] >> 1)) f(c, h[k][c], code[k] & 1);
-    }
-}
-
 // Gather the fct_adf_h levels z0..z0+C-1 of a node's edges (CSR slice [e0, e1), ascending edge
 // order) and hand each (value, second-endpoint flag) to `f(c, h, second)` in that order.
-// agent-coherent loads (read-only data another workgroup of this launch published: no L1 hit)
-template <int C>
-__device__ __forceinline__ void ldv_coh(const real *p, real (&v)[C])
-{
-#pragma unroll
-    for (int c = 0; c < C; c++) v[c] = __hip_atomic_load(p + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int C, int kBatch, bool COH = false, bool ODD = false, class F>
+template <int C, int kBatch, bool ODD = false, class F>
 __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
                                           const real *__restrict__ adf_h, int z0, int L, F &&f,
                                           bool last1 = false)
@@ -502,10 +373,7 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             if (z0 < (code[k] >> 1)) {
-                if constexpr (COH)
-                    ldv_coh<C>(adf_h + idx[k], h[k]);
-                else
-                    ldo_pre<C, ODD>(adf_h + idx[k], h[k], last1);
+                ldo_pre<C, ODD>(adf_h + idx[k], h[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;
@@ -621,9 +489,8 @@ __device__ __forceinline__ void b3h_groups(const int4 *__restrict__ einfo, int n
 // interface below a thread's levels is recomputed in-thread from plus/minus (the bottom interface
 // nlev-1 is never limited); the barrier orders every raw fct_adf_v read of the block before its
 // writes.
-// The node work of phase 2 for the block's G columns (records staged): see k_p2.  COH: fct_adf_h
-// read with agent-coherent loads (the persistent phase 2 publishes it inside the launch).
-template <int C, int KB, bool NT, bool COH>
+// The node work of phase 2 for the block's G columns (records staged): see k_p2.
+template <int C, int KB, bool NT>
 __device__ __forceinline__ void p2_node_work(const MeshPlanDev &mp, P2Args &a, const NodeRec *recs, int ncol,
                                              float invS)
 {
@@ -692,8 +559,8 @@ __device__ __forceinline__ void p2_node_work(const MeshPlanDev &mp, P2Args &a, c
             auto add = [&](int c, real h, int second) {
                 dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
             };
-            for_edges<C, KB, COH>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
-            if (ne > kRecEdge) for_edges<C, KB, COH>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
+            for_edges<C, KB>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add);
+            if (ne > kRecEdge) for_edges<C, KB>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add);
         }
     }
     __syncthreads();

@@ -77,22 +77,6 @@ Buffer *buf(void **h, const char *name)
     return b;
 }
 
-int *plan_edge_counters(const Plan *p, int ntr)
-{
-    if (ntr > p->cnt_tracers) {
-        p->edge_cnt = static_cast<int *>(p->cnt_mem.alloc(sizeof(int) * (size_t)std::max(p->dev.n_edges, 1) * ntr));
-        if (!p->edge_cnt) return nullptr;
-        p->cnt_tracers = ntr;
-    }
-    return p->edge_cnt;
-}
-
-int *plan_wf_state(const Plan *p)
-{
-    if (!p->wf_state) p->wf_state = static_cast<int *>(p->cnt_mem.alloc(sizeof(int) * (16 + (size_t)p->dev.wf_ntiles)));
-    return p->wf_state;
-}
-
 Buffer *need(void **h, size_t bytes, const char *name)
 {
     Buffer *b = buf(h, name);
@@ -697,36 +681,6 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             zdry[n] = zd;
             rptr[n + 1] = (int)ring.size();
         }
-        // does every owned node's cluster equal {n} + its edge neighbours, on the edges' levels?
-        // (the tuning build's edge-list phase 1, FESOM2_P1_EDGE)
-        if (F2A_TUNING && n_csr >= n_owned) {
-            bool same = true;
-            for (int n = 0; n < n_owned && same; n++) {
-                const int ne = ptr[n + 1] - ptr[n], nr = rptr[n + 1] - rptr[n];
-                if (nr != ne + 1) {
-                    same = false;
-                    break;
-                }
-                int self = -1, emax = 0;
-                for (int k = ptr[n]; k < ptr[n + 1]; k++) emax = std::max(emax, refs[k].code >> 1);
-                for (int r = rptr[n]; r < rptr[n + 1] && same; r++) {
-                    const RingRef rr = ring[r];
-                    if (rr.node == n) {
-                        self = rr.lev;
-                        continue;
-                    }
-                    bool found = false;
-                    for (int k = ptr[n]; k < ptr[n + 1]; k++)
-                        if (refs[k].other == rr.node) {
-                            found = (refs[k].code >> 1) == rr.lev;
-                            break;
-                        }
-                    same = found;
-                }
-                same = same && self == emax;
-            }
-            d.edge_cluster = same;
-        }
         d.ring_ptr = plan->mem.upload(rptr);
         d.ring = plan->mem.upload(ring);
         d.zdry = plan->mem.upload(zdry);
@@ -760,17 +714,6 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // plan option FESOM2_PATCH (nodes per patch; 1 = index order), read when the plan is built
         const char *env = getenv("FESOM2_PATCH");
         const int patch = env ? atoi(env) : (local_numbering ? 16384 : 4096);
-        // tuning build: FESOM2_SUBPATCH (compact BFS blobs of that many nodes inside a patch) and
-        // FESOM2_BLOB=1 (compact blobs of one p1v block: the next node is the unassigned patch
-        // neighbour with the most edges into the blob, so more edges have both endpoints in one p1v
-        // block and are limited there, see MeshPlanDev::int_ptr) -- both measured neutral
-        const int sub = knob("FESOM2_SUBPATCH", 0);
-        const int blob_g = knob("FESOM2_BLOB", 0) != 0 ? p1v_group_columns(nl) : 0;
-        std::vector<int> in_patch, bscore;
-        if (blob_g > 1) {
-            in_patch.assign(n_owned, -1);
-            bscore.assign(n_owned, 0);
-        }
         // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
         // tuning build
         const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);
@@ -832,70 +775,6 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     std::sort(cur.begin(), cur.end());
                 }
                 npatch++;
-                if (blob_g > 1 && (int)cur.size() > blob_g) {
-                    const int id = npatch;
-                    for (int v : cur) in_patch[v] = id;  // unassigned members of this patch
-                    std::vector<int> blob, cand;
-                    for (int v0 : cur) {  // seeds in the patch's order
-                        if (in_patch[v0] != id) continue;
-                        blob.assign(1, v0);
-                        in_patch[v0] = -2;
-                        cand.clear();
-                        auto touch = [&](int v) {
-                            for (int k = ptr[v]; k < ptr[v + 1]; k++) {
-                                const int w = other[k];
-                                if (w < n_owned && in_patch[w] == id) {
-                                    if (bscore[w]++ == 0) cand.push_back(w);
-                                }
-                            }
-                        };
-                        touch(v0);
-                        while ((int)blob.size() < blob_g && !cand.empty()) {
-                            size_t bi = 0;
-                            for (size_t q = 1; q < cand.size(); q++)
-                                if (bscore[cand[q]] > bscore[cand[bi]] ||
-                                    (bscore[cand[q]] == bscore[cand[bi]] && cand[q] < cand[bi]))
-                                    bi = q;
-                            const int w = cand[bi];
-                            cand.erase(cand.begin() + bi);
-                            bscore[w] = 0;
-                            in_patch[w] = -2;
-                            blob.push_back(w);
-                            touch(w);
-                        }
-                        for (int w : cand) bscore[w] = 0;
-                        std::sort(blob.begin(), blob.end());
-                        order.insert(order.end(), blob.begin(), blob.end());
-                    }
-                    continue;
-                }
-                if (sub > 1 && (int)cur.size() > sub) {
-                    // FESOM2_SUBPATCH: cut the patch into compact BFS blobs of `sub` nodes (the
-                    // fused kernels' columns per block), so a block's columns share their clusters
-                    std::vector<int> blob, rest(cur);
-                    std::vector<char> in(cur.size(), 1);
-                    auto idx = [&](int v) { return (int)(std::lower_bound(cur.begin(), cur.end(), v) - cur.begin()); };
-                    size_t pos = 0;
-                    for (size_t taken = 0; taken < cur.size();) {
-                        while (!in[pos]) pos++;
-                        blob.assign(1, cur[pos]);
-                        in[pos] = 0;
-                        for (size_t h = 0; h < blob.size() && (int)blob.size() < sub; h++)
-                            for (int k = ptr[blob[h]]; k < ptr[blob[h] + 1] && (int)blob.size() < sub; k++) {
-                                const int w = other[k];
-                                if (w >= n_owned) continue;
-                                const int q = idx(w);
-                                if (q < (int)cur.size() && cur[q] == w && in[q]) {
-                                    in[q] = 0;
-                                    blob.push_back(w);
-                                }
-                            }
-                        std::sort(blob.begin(), blob.end());
-                        order.insert(order.end(), blob.begin(), blob.end());
-                        taken += blob.size();
-                    }
-                    continue;
-                }
                 order.insert(order.end(), cur.begin(), cur.end());
             }
         }
@@ -935,83 +814,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             etaken[e] = 1;
             einfo.push_back(make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e));
         };
-        plan->owner_cum.assign(1, 0);
-        for (int v : order) {
+        for (int v : order)
             for (int k = ptr[v]; k < ptr[v + 1]; k++)
                 if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
-            plan->owner_cum.push_back((int)einfo.size());  // edges owned by positions < k+1
-        }
         for (int e = 0; e < n_edges; e++)
             if (!etaken[e]) push_edge(e);
-#if F2A_TUNING
-        // edges in owner order (the tuning build's chunked phase 2, node-centric b3h and fused p2h:
-        // an edge belongs to its first visited endpoint)
-        d.p_edge_owner = plan->mem.upload(einfo);
-        d.p_owner_cum = plan->mem.upload(plan->owner_cum);
-        if (!d.p_edge_owner || !d.p_owner_cum) return fail("device allocation for the edge order failed");
-        // persistent phase-2 plan (MeshPlanDev::wf_*): tiles of the fused kernels' G positions
-        {
-            const int WG = f2a::fused_group_columns(nl);
-            const int ntiles = (n_owned + WG - 1) / WG;
-            std::vector<int> pos(n_owned);
-            for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
-            int sf[f2a::kWfStreams + 1];
-            for (int x = 0; x <= f2a::kWfStreams; x++) sf[x] = (int)((long)x * ntiles / f2a::kWfStreams);
-            auto stream_of_tile = [&](int t) {
-                int x = 0;
-                while (t >= sf[x + 1]) x++;
-                return x;
-            };
-            std::vector<int> owner(n_edges, -1), cnt(ntiles + 1, 0);
-            std::vector<int4> cross;
-            for (int e = 0; e < n_edges; e++) {
-                const int n1 = m.edges[2 * (size_t)e] - 1, n2 = m.edges[2 * (size_t)e + 1] - 1;
-                const int t1 = n1 < n_owned ? pos[n1] / WG : -1, t2 = n2 < n_owned ? pos[n2] / WG : -1;
-                const int4 ei = make_int4(n1, n2, lev[e], e);
-                if (t1 >= 0 && t2 >= 0 && stream_of_tile(t1) != stream_of_tile(t2)) {
-                    cross.push_back(ei);
-                } else {
-                    owner[e] = t1 < 0 ? t2 : (t2 < 0 ? t1 : std::min(t1, t2));
-                    if (owner[e] >= 0) cnt[owner[e] + 1]++;
-                }
-            }
-            for (int t = 0; t < ntiles; t++) cnt[t + 1] += cnt[t];
-            std::vector<int4> wfe(cnt[ntiles]);
-            {
-                std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-                for (int e = 0; e < n_edges; e++)
-                    if (owner[e] >= 0)
-                        wfe[fill[owner[e]]++] = make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e);
-            }
-            std::vector<int> dptr(1, 0), deps;
-            for (int t = 0; t < ntiles; t++) {
-                const size_t d0 = deps.size();
-                for (int k = t * WG; k < std::min(n_owned, (t + 1) * WG); k++) {
-                    const int v = order[k];
-                    for (int q = ptr[v]; q < ptr[v + 1]; q++) {
-                        const int o = owner[refs[q].edge];
-                        if (o < 0 || o == t) continue;
-                        if (std::find(deps.begin() + d0, deps.end(), o) == deps.end()) deps.push_back(o);
-                    }
-                }
-                dptr.push_back((int)deps.size());
-            }
-            d.wf_G = WG;
-            d.wf_ntiles = ntiles;
-            d.wf_ncross = (int)cross.size();
-            for (int x = 0; x <= f2a::kWfStreams; x++) d.wf_stream_first[x] = sf[x];
-            d.wf_edges = plan->mem.upload(wfe);
-            d.wf_cross = plan->mem.upload(cross);
-            d.wf_edge_ptr = plan->mem.upload(cnt);
-            d.wf_dep_ptr = plan->mem.upload(dptr);
-            d.wf_deps = plan->mem.upload(deps);
-            if (!d.wf_edges || !d.wf_cross || !d.wf_edge_ptr || !d.wf_dep_ptr || !d.wf_deps)
-                return fail("device allocation for the persistent phase-2 plan failed");
-            if (knob("FESOM2_PLAN_STATS", 0))
-                fprintf(stderr, "fesom2-accelerate: wavefront G=%d tiles=%d cross edges=%zu deps/tile %.2f\n", WG, ntiles,
-                        cross.size(), (double)deps.size() / std::max(ntiles, 1));
-        }
-#endif
         // interior / boundary split for the exchange overlap (stable: processing order kept), the
         // interior part split again into edges crossing p1v blocks and edges inside one p1v block
         // (both endpoints among the same int_G positions: p1v limits those itself, see int_ptr)
@@ -1091,45 +898,6 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             for (int q = 0; q < kRecEdge && info[k].e0 + q < info[k].e1; q++) r.edge[q] = pedges[info[k].e0 + q];
         }
         d.node_rec = plan->mem.upload(recs);
-        // cluster staging plan for phase 1 (see MeshPlanDev::stage_*; the tuning build's
-        // FESOM2_P1_STAGE)
-        if (F2A_TUNING && with_ring) {
-            const int SG = f2a::fused_group_columns(nl);
-            std::vector<int> bptr(1, 0), bnodes;
-            std::vector<NodeRec> srecs(recs);
-            std::vector<RingRef> sring(pring);
-            int umax = 0;
-            for (int b0 = 0; b0 < n_owned; b0 += SG) {
-                const int base = (int)bnodes.size();
-                auto slot = [&](int v) {
-                    for (int q = base; q < (int)bnodes.size(); q++)
-                        if (bnodes[q] == v) return q - base;
-                    bnodes.push_back(v);
-                    return (int)bnodes.size() - 1 - base;
-                };
-                for (int k = b0; k < std::min(b0 + SG, n_owned); k++)
-                    for (int r = info[k].r0; r < info[k].r1; r++) sring[r].node = slot(pring[r].node);
-                for (int k = b0; k < std::min(b0 + SG, n_owned); k++)
-                    for (int q = 0; q < kRecRing && info[k].r0 + q < info[k].r1; q++)
-                        srecs[k].ring[q] = sring[info[k].r0 + q];
-                umax = std::max(umax, (int)bnodes.size() - base);
-                bptr.push_back((int)bnodes.size());
-            }
-            if (knob("FESOM2_PLAN_STATS", 0))
-                fprintf(stderr, "fesom2-accelerate: staging G=%d blocks=%zu union mean %.2f max %d, ring mean %.2f\n", SG,
-                        bptr.size() - 1, (double)bnodes.size() / std::max<size_t>(bptr.size() - 1, 1), umax,
-                        (double)pring.size() / std::max(n_owned, 1));
-            if (umax <= f2a::kMaxStage) {
-                d.stage_G = SG;
-                d.stage_max = umax;
-                d.blk_ptr = plan->mem.upload(bptr);
-                d.blk_nodes = plan->mem.upload(bnodes);
-                d.s_rec = plan->mem.upload(srecs);
-                d.s_ring = plan->mem.upload(sring);
-                if (!d.blk_ptr || !d.blk_nodes || !d.s_rec || !d.s_ring)
-                    return fail("device allocation for the staging plan failed");
-            }
-        }
 
         std::vector<char> interior_node(n_owned, 1);
         for (int n = 0; n < n_owned; n++)

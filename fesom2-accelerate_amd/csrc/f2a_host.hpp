@@ -155,19 +155,7 @@ struct Plan {
     int num_kernels = 10;     // stepwise phase 1 stops after this many reference steps
     bool has_ring = false;
     int lmax_edges = 0;
-    std::vector<int> owner_cum;  // [n_owned + 1]: edges owned by processing positions < k
-
-    // per-edge arrival counters of the fused b3h, grown to the largest tracer batch seen
-    mutable DeviceArrays cnt_mem;
-    mutable int *edge_cnt = nullptr;
-    mutable int cnt_tracers = 0;
-    // persistent phase-2 state: 8 tickets, timeout word, tile flags (zeroed before every launch)
-    mutable int *wf_state = nullptr;
 };
-// The plan's edge counters for ntr tracers (nullptr on allocation failure).
-int *plan_edge_counters(const Plan *p, int ntr);
-// The plan's persistent phase-2 state words (16 + tiles ints; nullptr on allocation failure).
-int *plan_wf_state(const Plan *p);
 
 // Node->edge CSR for nodes [0, n_csr) in ascending edge order; clusters for [0, n_owned) when the
 // element connectivity is present.  Validates every index; returns nullptr with `err` set.

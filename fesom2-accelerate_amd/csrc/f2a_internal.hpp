@@ -7,9 +7,9 @@
 #include <cstdint>
 #include <cstdlib>
 
-// The tuning build (make tuning -> lib/libfesom2-accelerate-tuning.so, F2A_TUNING=1) adds the
-// measured-and-rejected kernel variants (fct_ale_variants.hip) and reads the FESOM2_* A/B knobs
-// tools/sweep_env.sh sweeps.  The product library compiles every knob to its measured default:
+// The tuning build (make tuning -> lib/libfesom2-accelerate-tuning.so, F2A_TUNING=1) reads the
+// FESOM2_* A/B knobs tools/sweep_env.sh sweeps (other gather batches, wave counts, cache policies,
+// tile orders, timing-only ablations).  The product library compiles every knob to its measured default:
 // no environment variable changes its kernel selection (the plan options of get_plan aside,
 // which are read once when a mesh plan is built; INTEGRATION.md lists them).
 #ifndef F2A_TUNING
@@ -152,31 +152,11 @@ struct MeshPlanDev {
     int int_G = 0;                        // 0: no internal-edge lists
     const int *int_ptr = nullptr;
     const int4 *int_edges = nullptr;
-    const int4 *p_edge_owner = nullptr;   // the same edges in owner order (first visited endpoint)
-    const int *p_owner_cum = nullptr;     // [n_owned + 1]: edges owned by processing positions < k
-    // persistent phase 2 (launch_p2_wavefront): tiles of G positions, kWfStreams ticket streams of
-    // consecutive tiles; per tile the owned edges in wf_edges[wf_edge_ptr[t] ..), the earlier tiles
-    // whose edges it needs in wf_deps[wf_dep_ptr[t] ..); edges between streams pre-limited (wf_cross)
-    int wf_G = 0, wf_ntiles = 0, wf_ncross = 0;
-    int wf_stream_first[9] = {};
-    const int4 *wf_edges = nullptr, *wf_cross = nullptr;
-    const int *wf_edge_ptr = nullptr, *wf_dep_ptr = nullptr, *wf_deps = nullptr;
     // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
     int n_p2_interior = 0;
     int max_degree = 0;                   // most edges at one owned node
-    // every owned node's cluster is the node plus its edge neighbours, each on its edge's levels
-    // (a consistent triangulation): phase 1 gathers ttf/LO along the edge list
-    bool edge_cluster = false;
-    // phase-1 cluster staging: for block b (stage_G consecutive positions) the distinct cluster
-    // nodes blk_nodes[blk_ptr[b] .. blk_ptr[b+1]) are staged into LDS once; s_rec / s_ring are
-    // node_rec / p_ring with every cluster node replaced by its slot in the block's list
-    int stage_G = 0, stage_max = 0;       // stage_max = 0: staging off (no ring, or unions too large)
-    const int *blk_ptr = nullptr, *blk_nodes = nullptr;
-    const NodeRec *s_rec = nullptr;
-    const RingRef *s_ring = nullptr;
-    int *edge_cnt = nullptr;              // [n_edges * tracers] arrival counters of the fused b3h
 };
 
 // Batched tracers: `n` tracers whose per-tracer arrays follow each other in one buffer, `node`
@@ -187,7 +167,6 @@ struct MeshPlanDev {
 struct Tracers {
     int n = 1;
     size_t node = 0, lev = 0, edge = 0;
-    int chunk = 0;  // p1v: > 0 = XCD-chunked tracer tiles of that many column groups (group_tracer_chunked)
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().
@@ -226,8 +205,6 @@ inline size_t p1_lds_bytes(int G, int L, int vlimit, bool internal)
     return (2 + (vlimit != 1 ? 1 : 0)) * (size_t)G * L * sizeof(double) + (size_t)G * 192 +
            (internal ? p1_internal_lds_bytes() : 0);
 }
-// opt-in phase-1 variants (fct_ale_variants.hip): *handled = false when no switch selects one
-hipError_t launch_p1_variant(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool *handled);
 
 struct P2Args {
     int nl;
@@ -237,43 +214,21 @@ struct P2Args {
     real *adf_v, *adf_h, *del_v, *del_h;
     real dt;
     Tracers tr;
-    int n_owned = 0;          // fused b3h (edge_cnt set): owned-node bound for `other`
-    int *edge_cnt = nullptr;  // fused b3h: zeroed per-edge(-per-tracer) arrival counters
 };
 hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
-// c-horizontal with b3-horizontal folded in (split pass, FESOM2_P2H_FUSE): a.edge_cnt = the plan's
-// per-edge arrival counters (never reset: two arrivals per edge per pass), a.n_owned set, every node
-// of mp.max_degree <= kMaxFusedDegree; edges without an owned endpoint are not touched
-hipError_t launch_p2hf(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
-// b3-horizontal folded into the node kernel (a.edge_cnt zeroed, mp.max_degree <= kMaxFusedDegree):
-// every endpoint limits its edges' fluxes itself for c-horizontal, and the endpoint that arrives
-// last at an edge's counter -- after its block has read the raw column -- writes the limited
-// fct_adf_h.
-constexpr int kMaxFusedDegree = 32;
-constexpr int kWfStreams = 8;  // one ticket stream per XCD
-// persistent phase 2 (b3h + node kernel interleaved per tile; single tracer, no exchange overlap).
-// `state` = zeroed ints: [0, 8) tickets, [8] timeout, [16, 16 + wf_ntiles) tile flags.
-hipError_t launch_p2_wavefront(const MeshPlanDev &mp, const P2Args &a, int *state, hipStream_t s);
-hipError_t launch_p2_fused_b3h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
 // b3-horizontal over all local edges of the plan (edge groups, flat levels)
 hipError_t launch_b3h_fused(const MeshPlanDev &mp, int nl, int begin, int count, const real *plus,
                             const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
 // b3-horizontal over the interior edges crossing p1v blocks (mp.p_edge_ext)
 hipError_t launch_b3h_ext(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
                           const Tracers &tr, hipStream_t s);
-// chunk c's node kernel and the next chunk's b3h in one launch (node blocks first; one tracer)
-hipError_t launch_p2_b3h_chunk(const MeshPlanDev &mp, const P2Args &a, const int4 *einfo, int n_edges, hipStream_t s);
-// the same over an explicit edge list
-// b3-horizontal node-centric: the edges each processing position owns (p_edge_owner), the owner's
-// plus/minus loaded once for all of them; edges without an owned endpoint edge-centric
 // reference-sequence entries on the fused path: b3v and the c-step (cv + ch over the processing
 // order) with the production kernels' column-group shape
 hipError_t launch_b3v_cols(int n_owned, int nl, const int *nlev, const real *plus, const real *minus, real *adf_v,
                            hipStream_t s);
 hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s);
-hipError_t launch_b3h_nodes(const MeshPlanDev &mp, int nl, int owned_edges, int n_edges, const real *plus,
-                            const real *minus, real *adf_h, const Tracers &tr, hipStream_t s);
+// b3-horizontal over an explicit edge list ({node1, node2, lev, edge}, 0-based)
 hipError_t launch_b3h_edges(const int4 *einfo, int count, int nl, const real *plus, const real *minus,
                             real *adf_h, const Tracers &tr, hipStream_t s);
 // iter_yn phase 2 (docs/refactoring.md:227-229, :258-260, :265-290): node kernel = b3v writing
@@ -295,9 +250,6 @@ hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, cons
                            real *adf_h2, const Tracers &tr, hipStream_t s);
 // columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
 int group_columns(int L);
-// columns per block of the fused node kernels for nl levels (the staging plan's block size)
-int fused_group_columns(int nl);
-constexpr int kMaxStage = 64;  // most distinct cluster nodes a block stages
 
 // Stepwise kernels, one per reference step.
 hipError_t launch_a1(int n_nodes, int nl, const int *nlev_nod, const real *LO, const real *ttf,

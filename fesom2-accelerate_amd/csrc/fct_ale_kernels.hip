@@ -319,32 +319,15 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
 // reference entry sequence's fct_ale_pre_comm_acc_ in the fast mode: it has no del_ttf_advvert,
 // hnode, hnode_new or area; fct_ale_c_acc_ does cv).
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
-__device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G, float invS, int grp_in = -1,
-                                        const NodeRec *recs_in = nullptr)
+__device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G, float invS)
 {
     extern __shared__ real lds[];  // tvert max | tvert min | NodeRec[G]
-    // OPT & 256: a persistent block's tile (k_p1p): the column group and its records (already in LDS,
-    // prefetched by DMA during the previous tile) come from the caller
-    constexpr bool PERSIST = (OPT & 256) != 0;
-    // OPT & 128 (VERT): the block runs its G columns for every tracer of the batch in turn -- the
-    // records, the internal-edge entries and the slot geometry are set up once, and the shared mesh
-    // fields (area_inv, area, hnode, hnode_new) of the block's columns come back from L2 for the
-    // later tracers.  Otherwise tiles are (column group, tracer).
-    constexpr bool TLOOP = (OPT & 128) != 0;
-    static_assert(!TLOOP || VERT, "the tracer loop keeps every thread in every barrier: VERT forms only");
+    // tiles are (column group, tracer), tracer fastest (group_tracer)
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
-    int t = threadIdx.x;
-    // persistent: an opaque copy per tile, so nothing derived from the thread index is hoisted out of
-    // the caller's tile loop and kept live across it (registers = occupancy)
-    if constexpr (PERSIST) asm volatile("" : "+v"(t));
-    int tr0 = 0;
-    const int grp = PERSIST ? grp_in
-                    : TLOOP ? block_tile()
-                    : a0.tr.chunk > 0 ? group_tracer_chunked(a0.tr.n, (a0.n_owned + G - 1) / G, a0.tr.chunk, tr0)
-                                      : group_tracer(a0.tr.n, tr0, c_tracer_major & 1, c_tile_rev & 1);
-    if (grp < 0) return;  // a padding tile of the chunked grid (block-uniform, before any barrier)
+    const int t = threadIdx.x;
+    int tr = 0;
+    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, c_tile_rev & 1);
     const int first = grp * G;
-    const int ntl = TLOOP ? a0.tr.n : 1;
     const int ncol = min(G, a0.n_owned - first);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
     // after b2, from the plus/minus in LDS.  Wave 0 stages their entries and slot offsets (one
@@ -382,7 +365,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     // (behind the records and the internal-edge staging: p1_lds_bytes)
     real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
-    const NodeRec *recs = PERSIST ? recs_in : stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
+    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
         if (t < int_n)  // wave 0 (int_n <= kMaxInternal = kWave): lane t's entry lands at ie_ent[t]
             __builtin_amdgcn_global_load_lds(
@@ -394,9 +377,6 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     const int z0 = C * u;
     const bool last1 = ODD && z0 + 1 == L;
     const bool col = j < ncol;
-#pragma clang loop unroll(disable)
-    for (int it = 0; it < ntl; it++) {
-    const int tr = TLOOP ? it : tr0;
     P1Args a = a0;
     if (tr) {
         a.ttf += tr * a.tr.node;
@@ -407,12 +387,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         a.adf_h += tr * a.tr.edge;
         if (VERT && !(OPT & 64)) a.del_v += tr * a.tr.node;
     }
-    if (TLOOP && it > 0) __syncthreads();  // the previous tracer's LDS reads are done
-    // the column's record entries are re-read from LDS per tracer: an opaque copy of j keeps the
-    // compiler from hoisting all 40 of them into registers across the loop (occupancy)
-    int jr = j;
-    if constexpr (TLOOP) asm volatile("" : "+v"(jr));
-    const NodeRec &rec = recs[jr];
+    const NodeRec &rec = recs[j];
     NodeInfo ni{};
     if (col) ni = rec.info;
     const int Ln = ni.Ln;
@@ -427,27 +402,12 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     real v[C + 1];  // raw fct_adf_v at z0 .. z0+C (b1v; the VERT tail limits them)
 #pragma unroll
     for (int c = 0; c <= C; c++) v[c] = 0.;
-    real ai[C], e_dv[C], e_hn[C], e_hnn[C], e_ar[C];  // area_inv; OPT & 2: the tail's own streams
+    real ai[C];  // area_inv
 #pragma unroll
-    for (int c = 0; c < C; c++) ai[c] = e_dv[c] = e_hn[c] = e_hnn[c] = e_ar[c] = 0.;
-    // OPT & 8 (VERT, even L): the vertical tail's own L-stride streams (del_ttf_advvert, hnode,
-    // hnode_new) go global -> LDS by DMA (global_load_lds_dwordx4, no VGPRs) right after the records,
-    // lane-linear behind the NodeRecs; the first barrier's vmcnt(0) lands them
-    real *gl = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real));
-    const int gl_n = (int)blockDim.x * C;  // doubles per DMA region
+    for (int c = 0; c < C; c++) ai[c] = 0.;
     if (nw > 0) {
         b = (size_t)ni.n * L + z0;
         ab = (size_t)ni.n * a.nl + z0;
-        if constexpr (VERT && (OPT & 8) && C == 2 && !ODD) {
-            auto dma = [&](const real *src, real *dst) {
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                                 (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
-            };
-            real *w = gl + (threadIdx.x >> 6) * 64 * C;  // wave base: lane i lands at w + C*i
-            dma(a.del_v + b, w);
-            dma(a.hnode + b, w + gl_n);
-            dma(a.hnode_new + b, w + 2 * gl_n);
-        }
         if constexpr ((OPT & 4) != 0 && C == 2) {
             const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(a.adf_v + ab);  // one 16-B load at 8-B alignment
             v[0] = t.x;
@@ -473,17 +433,6 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         const size_t bl = b;  // (odd L: the last slot's pair reads one level past the column, ldo)
         ldo_pre<C, ODD>(a.LO + bl, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
         ldo_pre<C, ODD>(a.ttf + bl, tt, last1);
-        if constexpr (OPT & 1) {
-            // OPT & 1: the own-column streams of b2 and the vertical tail are issued with the first
-            // loads, so they land during the gathers instead of after the barriers
-            ld_nl<C, (OPT & 4) != 0>(a.area_inv + ab, nw, ai, 0.);
-            if constexpr (VERT && (OPT & 2)) {
-                ldo<C, ODD>(a.del_v + b, e_dv, last1);
-                ldo<C, ODD>(a.hnode + b, e_hn, last1);
-                ldo<C, ODD>(a.hnode_new + b, e_hnn, last1);
-                ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, e_ar, 1.);
-            }
-        }
 #pragma unroll
         for (int c = 0; c < C; c++)
             if (nr > 0 && z0 + c < ni.self_lev) {
@@ -491,28 +440,9 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
             }
         const int no = nr > 0 ? nr - 1 : 0;  // the other cluster nodes
-        // OPT & 512 (tuning build, FESOM2_P1V_DMA): one more cluster node / edge per round trip by LDS
-        // DMA (dma_base: 3 KB per wave behind the kernel's other LDS)
-        real *dma_w = nullptr;
-        if constexpr ((OPT & 512) != 0) {
-            const size_t off = (reinterpret_cast<size_t>(cmx + (VLIMIT != 1 ? G * L : 0)) + 15) & ~size_t(15);
-            dma_w = reinterpret_cast<real *>(off) + (size_t)(threadIdx.x >> 6) * 384;
-        }
-        if constexpr ((OPT & 512) != 0 && C == 2)
-            cluster_bound_dma<RB>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, dma_w, dma_w + 128,
-                                  (int)(threadIdx.x & 63));
-        else
         cluster_bound<C, RB, ODD>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
         if (no > kRecRing)
             cluster_bound<C, RB, ODD>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn, last1);
-        if constexpr ((OPT & 2) && VERT) {
-#pragma unroll
-            for (int c = 0; c < C; c++) {
-                real tv = e_dv[c] - tt[c] * e_hn[c];  // kernels/fct_ale_c_vertical.cu:9-12 order
-                e_dv[c] = tv + lo[c] * e_hnn[c];
-                e_ar[c] = a.dt / e_ar[c];
-            }
-        }
         auto add = [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
@@ -522,11 +452,8 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 m[c] += RMIN(0., h);
             }
         };
-        if constexpr ((OPT & 512) != 0 && C == 2)
-            for_edges_dma<EB>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, dma_w + 256, (int)(threadIdx.x & 63));
-        else
-        for_edges<C, EB, false, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
-        if (ne > kRecEdge) for_edges<C, EB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
+        for_edges<C, EB, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+        if (ne > kRecEdge) for_edges<C, EB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     }
     real *tvx = lds, *tvn = lds + G * L;
     const int q = j * L + z0;
@@ -541,7 +468,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     }
     __syncthreads();
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
-        if (it == 0 && t < kWave) {  // the DMA'd entries (landed: the barrier waited for vmcnt) -> slot offsets
+        if (t < kWave) {  // the DMA'd entries (landed: the barrier waited for vmcnt) -> slot offsets
             const int sl = t < int_n ? (ie_ent[t].w + C - 1) / C : 0;
             int incl = sl;
 #pragma unroll
@@ -558,12 +485,10 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
 #pragma unroll
     for (int c = 0; c < C; c++) op[c] = om[c] = 0.;
     if (nw > 0) {
-    if constexpr (!(OPT & 1)) {
-        if constexpr ((OPT & 4) != 0) ld_nl<C, true>(a.area_inv + ab, nw, ai, 0.);
-        else
+    if constexpr ((OPT & 4) != 0) ld_nl<C, true>(a.area_inv + ab, nw, ai, 0.);
+    else
 #pragma unroll
-        for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
-    }
+    for (int c = 0; c < C; c++) ai[c] = c < nw ? ld1_s<NT>(a.area_inv + ab + c) : 0.;
 #pragma unroll
     for (int c = 0; c < C; c++) {
         op[c] = om[c] = 0.;
@@ -651,7 +576,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 stv_s<C, true>(const_cast<real *>(a.adf_h) + (size_t)e.x * L + zi, out, nwi);
             }
         }
-        if (na <= 0) continue;  // (the last statement with barriers is behind)
+        if (na <= 0) return;  // (the last statement with barriers is behind)
         if (nw == 0) {  // no wet cell (nlevels_nod2D <= 1): only nz = 1 is limited, from memory
             b = (size_t)ni.n * L + z0;
             ab = (size_t)ni.n * a.nl + z0;
@@ -679,25 +604,11 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         real dv[C];
         if constexpr (OPT & 64) {
             (void)dv;
-        } else if ((OPT & 2) && nw > 0) {
-#pragma unroll
-            for (int c = 0; c < C; c++) dv[c] = e_dv[c] + (lim[c] - lim[c + 1]) * e_ar[c];
         } else if (nw > 0) {
             real del_v[C], hn[C], hnn[C], ar[C];
-            if constexpr ((OPT & 8) && C == 2 && !ODD) {
-                const real *me = gl + C * threadIdx.x;
-#pragma unroll
-                for (int c = 0; c < C; c++) {
-                    del_v[c] = me[c];
-                    hn[c] = me[gl_n + c];
-                    hnn[c] = me[2 * gl_n + c];
-                }
-            } else {
-                const size_t bl = b;
-                ldo_s_pre<C, NT, ODD>(a.del_v + bl, del_v, last1);
-                ldo_s_pre<C, NT, ODD>(a.hnode + bl, hn, last1);
-                ldo_s_pre<C, NT, ODD>(a.hnode_new + bl, hnn, last1);
-            }
+            ldo_s_pre<C, NT, ODD>(a.del_v + b, del_v, last1);
+            ldo_s_pre<C, NT, ODD>(a.hnode + b, hn, last1);
+            ldo_s_pre<C, NT, ODD>(a.hnode_new + b, hnn, last1);
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
 #pragma unroll
             for (int c = 0; c < C; c++) {
@@ -721,7 +632,6 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         if constexpr (!(OPT & 64))
             if (nw > 0) stv_s<C, NT>(a.del_v + b, dv, nw);
     }
-    }  // tracers
 }
 
 template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT = false, int OPT = 0, bool ODD = false>
@@ -730,79 +640,6 @@ __global__ __launch_bounds__(1024) void k_p1(MeshPlanDev mp, P1Args a, int G, fl
     p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
 
-#if F2A_TUNING
-// Persistent p1v (tuning build, FESOM2_P1V_PERSIST=1): a grid of resident blocks, block k of XCD x
-// (blocks are dealt to the XCDs round-robin) runs the column groups start_x + k, + B, + 2B, ... of
-// its XCD's contiguous range (B blocks per XCD), so the XCDs sweep their ranges as with one block per
-// group.  While a tile runs, the next tile's NodeRecs go global -> LDS by DMA into the other record
-// buffer (landed by the tile's first barrier): the dependent records round trip at the head of every
-// block's chain is hidden.  One tracer, vlimit 1, level pairs.  The arguments are re-read from the
-// kernarg segment every tile (an opaque pointer), so the compiler cannot keep the ~60 argument words
-// live across the tile loop (SGPR spills into VGPRs would cost the occupancy the body needs).
-struct P1PArgs {
-    MeshPlanDev mp;
-    P1Args a;
-    int G, rec1_off;
-    float invS;
-};
-
-template <int OPT, bool ODD>
-__device__ __forceinline__ void p1p_body()
-{
-    extern __shared__ real lds[];
-    typedef const __attribute__((address_space(4))) P1PArgs *KArgs;
-    KArgs ka = (KArgs)(__builtin_amdgcn_kernarg_segment_ptr());
-    const int G = ka->G, L = ka->a.nl - 1, n_owned = ka->a.n_owned;
-    const int groups = (n_owned + G - 1) / G;
-    const int q = groups >> 3, r = groups & 7, x = blockIdx.x & 7, k = blockIdx.x >> 3;
-    const int start = x * q + (x < r ? x : r), len = q + (x < r ? 1 : 0);
-    const int B = (int)(gridDim.x >> 3);
-    if (k >= len) return;  // block-uniform, before any barrier
-    constexpr int kChunks = sizeof(NodeRec) / 16;
-    {  // the first tile's records: plain loads + barrier
-        const int first = (start + k) * G, ncol = min(G, n_owned - first);
-        stage_records(ka->mp.node_rec, first, ncol, lds + 2 * G * L);
-    }
-    // loop state in SGPRs only (readfirstlane): every VGPR the loop carried would cost the body
-    // occupancy
-#pragma clang loop unroll(disable)
-    for (int i = 0;; i++) {
-        const int j = __builtin_amdgcn_readfirstlane(k + i * B);
-        KArgs kt = ka;
-        asm volatile("" : "+s"(kt));  // re-read the arguments for this tile
-        MeshPlanDev mp;
-        __builtin_memcpy(&mp, (const MeshPlanDev *)&kt->mp, sizeof mp);
-        P1Args a;
-        __builtin_memcpy(&a, (const P1Args *)&kt->a, sizeof a);
-        const int g = start + j;
-        const bool more = j + B < len;
-        const int cur = __builtin_amdgcn_readfirstlane((i & 1) ? kt->rec1_off : 2 * G * L);
-        const int nxt = __builtin_amdgcn_readfirstlane((i & 1) ? 2 * G * L : kt->rec1_off);
-        if (more) {  // next tile's records into the other buffer (wave w: bytes [1024 w, 1024 w + 1024))
-            const int first_n = (g + B) * G, ncol_n = min(G, n_owned - first_n);
-            const int w = (int)(threadIdx.x >> 6), idx = (int)threadIdx.x;
-            if (idx < ncol_n * kChunks)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(reinterpret_cast<const char *>(mp.node_rec + first_n) + 16 * idx),
-                    (__attribute__((address_space(3))) void *)(reinterpret_cast<char *>(lds + nxt) + 1024 * w), 16, 0, 0);
-        }
-        p1_body<1, 2, 2, 2, true, true, OPT | 256, ODD>(mp, a, G, kt->invS, g, reinterpret_cast<const NodeRec *>(lds + cur));
-        if (!more) break;
-        __syncthreads();  // the tile's LDS reads are done before the next one writes
-    }
-}
-template <int OPT, bool ODD>
-__global__ __launch_bounds__(1024) void k_p1p(P1PArgs)
-{
-    p1p_body<OPT, ODD>();
-}
-// held to 8 waves/SIMD (6 blocks per CU as the product p1v; the tile loop's extra registers spill)
-template <int OPT, bool ODD>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_p1p8(P1PArgs)
-{
-    p1p_body<OPT, ODD>();
-}
-#endif
 
 // p1 held to W waves/SIMD (amdgpu_waves_per_eu): the register allocator trades a few spills for
 // occupancy where a form sits just above a VGPR step (65 VGPRs = 7 waves, 74 = 6)
@@ -813,13 +650,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(W))) void 
     p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
 }
 
-// the tracer-loop form (OPT & 128, tuning build) held to 7 waves/SIMD (it spills there)
-template <int VLIMIT, int C, int RB, int EB, bool NT, bool VERT, int OPT, bool ODD = false>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(7))) void k_p1t(MeshPlanDev mp, P1Args a, int G,
-                                                                                       float invS)
-{
-    p1_body<VLIMIT, C, RB, EB, NT, VERT, OPT, ODD>(mp, a, G, invS);
-}
 
 // Phase 2, horizontal half (after the exchange, with b3h): c-horizontal only (see k_p1 VERT).
 template <int C, int KB, bool NT, bool PAIR = false, bool ODD = false>
@@ -859,8 +689,8 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     auto add = [&](int c, real h, int second) {
         dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
     };
-    for_edges<C, KB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
-    if (ne > kRecEdge) for_edges<C, KB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
+    for_edges<C, KB, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+    if (ne > kRecEdge) for_edges<C, KB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     stv_s<C, NT>(a.del_h + b, dh, nw);
 }
 
@@ -1092,8 +922,8 @@ __global__ __launch_bounds__(1024) void k_c(MeshPlanDev mp, P2Args a, int G, flo
     auto add = [&](int c, real h, int second) {
         dh[c] = second ? dh[c] - h * dta[c] : dh[c] + h * dta[c];  // docs/refactoring.md:311-312
     };
-    for_edges<C, KB, false, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
-    if (ne > kRecEdge) for_edges<C, KB, false, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
+    for_edges<C, KB, ODD>(recs[j].edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
+    if (ne > kRecEdge) for_edges<C, KB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
     stv<C>(a.del_v + b, dv, nw);
     stv<C>(a.del_h + b, dh, nw);
 }
@@ -1116,7 +946,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
     }
     const int ncol = min(G, a.count - first);
     const NodeRec *recs = stage_records(a.nodes, first, ncol, lds);
-    p2_node_work<C, KB, NT, false>(mp, a, recs, ncol, invS);
+    p2_node_work<C, KB, NT>(mp, a, recs, ncol, invS);
 }
 
 // iter_yn phase 2, nodes (see P2IterArgs).  Every slot of a column also copies fct_adf_v2 into
@@ -1441,15 +1271,9 @@ static hipError_t p1_launch_tuning(const MeshPlanDev &mp, const P1Args &a, hipSt
 }
 #endif
 
-int fused_group_columns(int nl)
-{
-    const int L = nl - 1;
-    return group_columns(L / levels_per_thread(L));
-}
-
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
-    if (odd_pairs(a.nl - 1) && a.vlimit == 1 && !knob("FESOM2_P1_EDGE", 0) && !knob("FESOM2_P1_STAGE", 0)) {
+    if (odd_pairs(a.nl - 1) && a.vlimit == 1) {
         const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
@@ -1458,11 +1282,7 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
     const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
 #if F2A_TUNING
-    // opt-in phase-1 variants (fct_ale_variants.hip), other gather batches (FESOM2_P1_BATCH =
-    // 10*RB + EB), cache policies
-    bool handled = false;
-    const hipError_t ve = launch_p1_variant(mp, a, s, &handled);
-    if (handled) return ve;
+    // other gather batches (FESOM2_P1_BATCH = 10*RB + EB), cache policies
     switch (knob("FESOM2_P1_BATCH", 22)) {
     case 44: return C == 2 ? p1_launch_tuning<2, 4, 4>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 4, 4>(mp, a, s, G, S, groups);
     case 24: return C == 2 ? p1_launch_tuning<2, 2, 4>(mp, a, s, G, S, groups) : p1_launch_tuning<1, 2, 4>(mp, a, s, G, S, groups);
@@ -1500,45 +1320,15 @@ static int p1v_launch_G(int nl, int vlimit)
 }
 
 // the launch_p1v forms with the internal-edge tail: the plan built the lists for this block size
-// (in the tuning build also the default load placement, and no phase-2 variant that limits every
-// edge itself)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 {
     return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit >= 1 && a.vlimit <= 3 &&
-           knob("FESOM2_P1V_B3H", 1) != 0 && knob("FESOM2_P1V_EARLY", 0) == 0 && !knob("FESOM2_P2H_FUSE", 0) &&
-           !knob("FESOM2_B3H_NODE", 0) && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
+           knob("FESOM2_P1V_B3H", 1) != 0 && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
 }
 
-#if F2A_TUNING
-// Batched tracers at vlimit 1 in level pairs: one block runs its G columns for every tracer in turn
-// (k_p1t, OPT & 128), XOPT = 64 without c-vertical; FESOM2_P1V_TLOOP=1 (tuning build).  Measured
-// 6 x 1.2M x 80: p1v 15.6 ms against 13.3 ms with a tile per (column group, tracer): the loop keeps
-// the tracer-independent state and the per-tracer pointers live (94 VGPRs, 5 waves/SIMD; bounded to
-// 7 waves it spills).  false: not selected, or not this shape.
-template <int XOPT>
-static bool launch_p1v_tloop(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in, hipError_t *err)
-{
-    const int L = a.nl - 1;
-    const bool odd = odd_pairs(L);
-    if (a.tr.n < 2 || a.vlimit != 1 || !knob("FESOM2_P1V_TLOOP", 0) || !(odd || levels_per_thread(L) == 2)) return false;
-    const int S = (L + 1) / 2, G = group_columns(S);
-    const long groups = (long)(a.n_owned + G - 1) / G;
-    const size_t lds = p1_lds_bytes(G, L, 1, in);
-    const float inv = 1.0f / (float)S;
-    *err = [&]() -> hipError_t {
-        if (odd) {
-            if (in) F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 52 | 128 | XOPT, true>), groups, G, S, lds, s, mp, a, G, inv);
-            F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 4 | 128 | XOPT, true>), groups, G, S, lds, s, mp, a, G, inv);
-        }
-        if (in) F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 52 | 128 | XOPT>), groups, G, S, lds, s, mp, a, G, inv);
-        F2A_LAUNCH_GROUPS((k_p1t<1, 2, 2, 2, true, true, 4 | 128 | XOPT>), groups, G, S, lds, s, mp, a, G, inv);
-    }();
-    return true;
-}
-#endif
 
 #if F2A_TUNING
-// every measured form of p1v (FESOM2_NT bit 2, FESOM2_P1V_EARLY, FESOM2_NL_PAIR, FESOM2_P1V_INT_DMA)
+// the measured forms of p1v (FESOM2_NT bit 2, FESOM2_NL_PAIR, FESOM2_P1V_INT_DMA)
 static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipStream_t s, bool in)
 {
     const int L = a.nl - 1;
@@ -1572,10 +1362,9 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
-    // OPT bits of k_p1 (VERT): 1 area_inv issued with the first loads, 2 + the tail's own streams
-    // (both measured slower: VGPRs), 4 16-B loads/stores of the stride-nl arrays (ld_nl, default),
-    // 8 the tail's streams staged into LDS by DMA, 16 the block-internal edges' b3-horizontal
-    const int early = knob("FESOM2_P1V_EARLY", 0) | (knob("FESOM2_NL_PAIR", 1) ? 4 : 0);
+    // OPT bits of k_p1 (VERT): 4 16-B loads/stores of the stride-nl arrays (ld_nl, default), 16 the
+    // block-internal edges' b3-horizontal, 32 their entries staged by DMA
+    const int early = knob("FESOM2_NL_PAIR", 1) ? 4 : 0;
     const bool nt = (knob("FESOM2_NT", 6) & 4) != 0;
     if (a.vlimit != 1 && C == 2 && early == 4 && nt) {
         if (in && a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, true, true, 20>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1601,15 +1390,8 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
     if (C == 2) {
         if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
         if (a.vlimit == 3) F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
-        if (early == 1) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 1>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 4 && nt) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
         if (early == 4) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4>), groups, G, S, lds, s, mp, a, G, invS);
-        if (early == 5) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 5>), groups, G, S, lds, s, mp, a, G, invS);
-        if (early == 12) {
-            const size_t lds_dma = lds + 3 * (size_t)threads_for(G, S) * 2 * sizeof(real);
-            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 12>), groups, G, S, lds_dma, s, mp, a, G, invS);
-        }
-        if (early & 2) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 7>), groups, G, S, lds, s, mp, a, G, invS);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
     if (a.vlimit == 2) F2A_LAUNCH_GROUPS((k_p1<2, 1, 2, 2, false, true>), groups, G, S, lds, s, mp, a, G, invS);
@@ -1623,85 +1405,6 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     if (!a.area || !a.hnode || !a.hnode_new || !a.del_v) return hipErrorInvalidValue;
     const bool in = p1v_limits_internal(mp, a);
 #if F2A_TUNING
-    hipError_t err;
-    if (launch_p1v_tloop<0>(mp, a, s, in, &err)) return err;
-    // FESOM2_TRACER_CHUNK = K: batched tracers in XCD-chunked tiles of K column groups
-    if (const int K = knob("FESOM2_TRACER_CHUNK", 0); K > 0 && a.tr.n > 1 && a.vlimit == 1) {
-        const int L = a.nl - 1;
-        const bool odd = odd_pairs(L);
-        if (odd || levels_per_thread(L) == 2) {
-            P1Args b = a;
-            b.tr.chunk = K;
-            const int S = (L + 1) / 2, G = group_columns(S);
-            const long gx = ((long)(a.n_owned + G - 1) / G + 7) / 8;
-            const long groups = 8 * gx * a.tr.n;
-            const size_t lds = p1_lds_bytes(G, L, 1, in);
-            const float inv = 1.0f / (float)S;
-            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52, true>), groups, G, S, lds, s, mp, b, G, inv);
-            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, b, G, inv);
-            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52>), groups, G, S, lds, s, mp, b, G, inv);
-            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4>), groups, G, S, lds, s, mp, b, G, inv);
-        }
-    }
-    // FESOM2_P1V_PERSIST = 1: persistent blocks with the next tile's records prefetched (k_p1p)
-    if (knob("FESOM2_P1V_PERSIST", 0) && a.vlimit == 1 && a.tr.n == 1) {
-        const int L = a.nl - 1;
-        const bool odd = odd_pairs(L);
-        if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S);
-            const long groups = (long)(a.n_owned + G - 1) / G;
-            const size_t lds0 = p1_lds_bytes(G, L, 1, in);
-            const int rec1_off = (int)((lds0 + 15) / 16 * 16 / sizeof(real));
-            const size_t lds = rec1_off * sizeof(real) + (size_t)G * sizeof(NodeRec);
-            const unsigned threads = threads_for(G, S);
-            auto launch = [&](const void *fn, auto kern) -> hipError_t {
-                int per_cu = 0, dev = 0;
-                hipDeviceProp_t prop;
-                if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)threads, lds) != hipSuccess || per_cu < 1)
-                    return hipErrorInvalidValue;
-                long grid = (long)per_cu * prop.multiProcessorCount / 8 * 8;
-                grid = std::min(grid, (groups + 7) / 8 * 8);
-                if (grid < 8) grid = 8;
-                init_swizzle();
-                P1PArgs pa{mp, a, G, rec1_off, 1.0f / (float)S};
-                hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), lds, s, pa);
-                return hipGetLastError();
-            };
-            if (knob("FESOM2_P1V_PERSIST", 0) == 2) {
-                if (odd && in) return launch((const void *)k_p1p8<52, true>, k_p1p8<52, true>);
-                if (odd) return launch((const void *)k_p1p8<4, true>, k_p1p8<4, true>);
-                if (in) return launch((const void *)k_p1p8<52, false>, k_p1p8<52, false>);
-                return launch((const void *)k_p1p8<4, false>, k_p1p8<4, false>);
-            }
-            if (odd && in) return launch((const void *)k_p1p<52, true>, k_p1p<52, true>);
-            if (odd) return launch((const void *)k_p1p<4, true>, k_p1p<4, true>);
-            if (in) return launch((const void *)k_p1p<52, false>, k_p1p<52, false>);
-            return launch((const void *)k_p1p<4, false>, k_p1p<4, false>);
-        }
-    }
-    // FESOM2_P1V_DMA = 1: one more cluster node and edge per gather round trip through LDS DMA
-    if (knob("FESOM2_P1V_DMA", 0) && a.vlimit == 1) {
-        const int L = a.nl - 1;
-        const bool odd = odd_pairs(L);
-        if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S);
-            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-            const unsigned threads = threads_for(G, S);
-            const size_t lds = (p1_lds_bytes(G, L, 1, in) + 15) / 16 * 16 + (size_t)(threads / 64) * 3072;
-            const float inv = 1.0f / (float)S;
-            if (knob("FESOM2_P1V_DMA", 0) == 2) {  // held to 8 waves/SIMD
-                if (odd && in) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
-                if (odd) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 4 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
-                if (in) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 512>), groups, G, S, lds, s, mp, a, G, inv);
-                F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 4 | 512>), groups, G, S, lds, s, mp, a, G, inv);
-            }
-            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
-            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
-            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512>), groups, G, S, lds, s, mp, a, G, inv);
-            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512>), groups, G, S, lds, s, mp, a, G, inv);
-        }
-    }
     // FESOM2_P1V_BATCH = 10*RB + EB: the production forms with other gather batches (cluster nodes /
     // edges per round trip; 22 = the product's)
     if (const int B = knob("FESOM2_P1V_BATCH", 22); B != 22 && a.vlimit == 1) {
@@ -1809,10 +1512,6 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     const bool in = p1v_limits_internal(mp, a);
-#if F2A_TUNING
-    hipError_t err;
-    if (launch_p1v_tloop<64>(mp, a, s, in, &err)) return err;
-#endif
     const int L = a.nl - 1;
     if (odd_pairs(L)) {
         const int S = (L + 1) / 2, G = group_columns(S);

@@ -637,78 +637,8 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                   dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
-    // b3-horizontal as its own edge kernel, then the node kernel.  The tuning build's measured
-    // alternatives: b3h folded into the node kernel (FESOM2_FUSE_B3H), phase 2 as one
-    // persistent launch (FESOM2_P2_WF), chunked phase 2 (FESOM2_P2_CHUNK / FESOM2_P2_MERGE).
-    [[maybe_unused]] const bool fuse = F2A_TUNING && knob("FESOM2_FUSE_B3H", 0) != 0 && d.max_degree <= f2a::kMaxFusedDegree;
-#if F2A_TUNING
-    if (fuse) {
-        a.n_owned = N;
-        a.edge_cnt = plan_edge_counters(plan, ntr);
-        if (!a.edge_cnt ||
-            !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
-            return;
-        if (!run("fct_ale_p2_b3h", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
-    } else if (knob("FESOM2_P2_WF", 0) && !comm && ntr == 1 && d.wf_ntiles > 0 && d.wf_G == f2a::fused_group_columns(NL)) {
-        // phase 2 as one persistent launch (b3h and the node kernel interleaved per tile)
-        int *state = plan_wf_state(plan);
-        if (!state || !ok(hipMemsetAsync(state, 0, sizeof(int) * (16 + (size_t)d.wf_ntiles), st), "hipMemsetAsync(wf)"))
-            return;
-        f2a::P2Args aw = a;
-        aw.nodes = d.node_rec;
-        aw.count = N;
-        if (!run("fct_ale_p2_wavefront", st, [&] { return f2a::launch_p2_wavefront(d, aw, state, st); })) return;
-    } else if (const int chunk = knob("FESOM2_P2_CHUNK", 0);
-               chunk > 0 && !comm && d.p_edge_owner && (int)plan->owner_cum.size() == N + 1) {
-        // FESOM2_P2_CHUNK=n: phase 2 in chunks of n nodes of the processing order -- b3h on the edges
-        // the chunk owns, then the node kernel on its nodes, so the limited fct_adf_h and plus/minus
-        // are re-read from the Infinity Cache (every node's edges belong to its own or an earlier
-        // chunk).  Measured break-even at 60k-node chunks (p2 -15 %, b3h +11 % from 2 x 20
-        // launches); two-stream pipelining of the chunks was slower.
-        const bool merge = knob("FESOM2_P2_MERGE", 0) && ntr == 1 &&
-                           (NL - 1) % 2 == 0;
-        auto edge_range = [&](int c0) {
-            const int c1 = std::min(N, c0 + chunk);
-            return std::make_pair(plan->owner_cum[c0], plan->owner_cum[c1] + (c1 == N ? E - plan->owner_cum[N] : 0));
-        };
-        if (merge) {
-            // b3h(0); then node kernel (c) + b3h(c+1) per launch; the last node kernel alone
-            const auto r0 = edge_range(0);
-            if (!run("fct_ale_b3_horizontal", st, [&] {
-                    return f2a::launch_b3h_edges(d.p_edge_owner + r0.first, r0.second - r0.first, NL, dptr<real>(bplus),
-                                                 dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
-                }))
-                return;
-            for (int c0 = 0; c0 < N; c0 += chunk) {
-                f2a::P2Args ac = a;
-                ac.nodes = d.node_rec + c0;
-                ac.count = std::min(N, c0 + chunk) - c0;
-                if (c0 + chunk < N) {
-                    const auto r = edge_range(c0 + chunk);
-                    if (!run("fct_ale_p2_b3h_chunk", st, [&] {
-                            return f2a::launch_p2_b3h_chunk(d, ac, d.p_edge_owner + r.first, r.second - r.first, st);
-                        }))
-                        return;
-                } else if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, ac, st); })) {
-                    return;
-                }
-            }
-        } else
-        for (int c0 = 0; c0 < N; c0 += chunk) {
-            const int c1 = std::min(N, c0 + chunk);
-            const int e0 = plan->owner_cum[c0], e1 = plan->owner_cum[c1] + (c1 == N ? E - plan->owner_cum[N] : 0);
-            if (!run("fct_ale_b3_horizontal", st, [&] {
-                    return f2a::launch_b3h_edges(d.p_edge_owner + e0, e1 - e0, NL, dptr<real>(bplus), dptr<real>(bminus),
-                                                 dptr<real>(badfh), a.tr, st);
-                }))
-                return;
-            f2a::P2Args ac = a;
-            ac.nodes = d.node_rec + c0;
-            ac.count = c1 - c0;
-            if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, ac, st); })) return;
-        }
-    } else
-#endif
+    // b3-horizontal as its own edge kernel, then the node kernel (the alternatives measured slower:
+    // DESIGN.md §3)
     {
         if (!run("fct_ale_b3_horizontal", st, [&] {
                 return f2a::launch_b3h_fused(d, NL, 0, e_first, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
@@ -721,11 +651,6 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
         a.nodes = d.p2_rec + n_first;
         a.count = N - n_first;
-#if F2A_TUNING
-        if (fuse) {
-            if (!run("fct_ale_p2_b3h_boundary", st, [&] { return f2a::launch_p2_fused_b3h(d, a, st); })) return;
-        } else
-#endif
         {
             if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
                     return f2a::launch_b3h_fused(d, NL, e_first, E - e_first, dptr<real>(bplus), dptr<real>(bminus),
@@ -796,53 +721,9 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), nullptr, nullptr, nullptr, nullptr,
                   dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
-#if F2A_TUNING
-    // FESOM2_P2H_FUSE=1 (tuning build): b3-horizontal folded into the c-horizontal node kernel
-    // (k_p2hf, arrival counters decide which endpoint stores the limited flux).  The counters are
-    // zeroed at every pass: a pass that stopped between its launches, or two passes on the same mesh
-    // on two streams, would otherwise leave their parity wrong (one mesh, one stream at a time).
-    if (!ip && knob("FESOM2_P2H_FUSE", 0) != 0 && d.max_degree <= f2a::kMaxFusedDegree &&
-        (int)plan->owner_cum.size() == N + 1) {
-        a.n_owned = N;
-        a.edge_cnt = plan_edge_counters(plan, ntr);
-        if (!a.edge_cnt ||
-            !ok(hipMemsetAsync(a.edge_cnt, 0, sizeof(int) * (size_t)std::max(E, 1) * ntr, st), "hipMemsetAsync(edge counters)"))
-            return;
-        const int owned_edges = plan->owner_cum.back();  // edges with an owned endpoint come first
-        if (!run("fct_ale_p2h_b3h", st, [&] { return f2a::launch_p2hf(d, a, st); })) return;
-        if (exch) {
-            if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
-            a.nodes = d.p2_rec + n_first;
-            a.count = N - n_first;
-            if (!run("fct_ale_p2h_b3h_boundary", st, [&] { return f2a::launch_p2hf(d, a, st); })) return;
-        }
-        if (owned_edges < E &&  // edges without an owned endpoint (none in a FESOM partition)
-            !run("fct_ale_b3_horizontal", st, [&] {
-                return f2a::launch_b3h_edges(d.p_edge_owner + owned_edges, E - owned_edges, NL, dptr<real>(bplus),
-                                             dptr<real>(bminus), dptr<real>(badfh), a.tr, st);
-            }))
-            return;
-        mark_internal(badfh, nullptr, st);
-        *alg_state = 9;
-        if (!g_resident && (!d2h_async(badfh, st) || !d2h_async(bdh, st))) *alg_state = 0;
-        return;
-    }
-    // FESOM2_B3H_NODE=1 (tuning build, no exchange): b3h node-centric over the owner order -- exact,
-    // measured 3-17 % slower than the edge-centric two-groups-per-block kernel
-    const bool b3h_nodes = !ip && !exch && d.p_owner_cum && knob("FESOM2_B3H_NODE", 0) != 0;
-#else
-    const bool b3h_nodes = false;
-#endif
     const f2a::MeshPlanDev &de = ip ? ip->dev : d;  // the edge lists b3h runs on
     const int eb = de.n_edge_interior;               // boundary edges (a halo endpoint): [eb, E)
     if (!run("fct_ale_b3_horizontal", st, [&] {
-#if F2A_TUNING
-            if (b3h_nodes)
-                return f2a::launch_b3h_nodes(d, NL, plan->owner_cum.back(), E, dptr<real>(bplus), dptr<real>(bminus),
-                                             dptr<real>(badfh), a.tr, st);
-#else
-            (void)b3h_nodes;
-#endif
             if (ip) {  // interior edges crossing p1v blocks; without an exchange the boundary ones too
                 const hipError_t e =
                     f2a::launch_b3h_ext(de, NL, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh), a.tr, st);

@@ -17,6 +17,12 @@ for p in (os.path.join(ROOT, "fesom2-accelerate_amd"), os.path.join(ROOT, "oracl
         sys.path.insert(0, p)
 
 
+# The tuning build's knob tests (tests/test_gpu_tuning.py) run only when FESOM2_LIB_NAME selects that
+# library; otherwise they are not collected at all, so product runs report no skips for them.
+collect_ignore = [] if os.environ.get("FESOM2_LIB_NAME") == "libfesom2-accelerate-tuning.so" else \
+    ["test_gpu_tuning.py"]
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
     config.addinivalue_line("markers", "slow: long-running (full-size meshes)")
