@@ -573,8 +573,23 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }
 
+PlanShape plan_shape(bool batched)
+{
+    PlanShape s;
+    const char *patch = getenv(batched ? "FESOM2_BATCH_PATCH" : "FESOM2_PATCH");
+    if (patch) s.patch = std::max(1, atoi(patch));  // 0 or 1: index order
+    if (batched) {
+        const char *gs = getenv("FESOM2_BATCH_GROUP_SHIFT");
+        if (!patch) s.patch = -1024;  // 1024 nodes where the numbering has locality (see build_plan)
+        s.gshift = gs ? atoi(gs) : -1;
+    } else {
+        s.gshift = knob("FESOM2_GROUP_SHIFT", 0);  // tuning build A/B
+    }
+    return s;
+}
+
 std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
-                                 int n_csr, int nl, std::string &err)
+                                 int n_csr, int nl, const PlanShape &shape, std::string &err)
 {
     auto plan = std::make_unique<Plan>();
     // plan option FESOM2_NUM_KERNELS: the stepwise path stops phase 1 after that many reference
@@ -585,6 +600,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     d.n_total = n_total;
     d.n_edges = n_edges;
     d.nl = nl;
+    d.gshift = shape.gshift;
     const int L = nl - 1;
     char msg[256];
     auto fail = [&](const char *s) {
@@ -711,9 +727,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 local_numbering = gap[gap.size() / 2] <= std::max(n_owned / 64, 64);
             }
         }
-        // plan option FESOM2_PATCH (nodes per patch; 1 = index order), read when the plan is built
-        const char *env = getenv("FESOM2_PATCH");
-        const int patch = env ? atoi(env) : (local_numbering ? 16384 : 4096);
+        // nodes per patch (1 = index order): the shape's (plan options FESOM2_PATCH /
+        // FESOM2_BATCH_PATCH), else by numbering; -k: k nodes for a numbering with locality
+        const int patch = shape.patch > 0 ? shape.patch
+                          : (local_numbering ? (shape.patch < 0 ? -shape.patch : 16384) : 4096);
         // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
         // tuning build
         const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);
@@ -831,7 +848,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
         const char *ienv = getenv("FESOM2_P1V_B3H");
         if (ienv ? atoi(ienv) != 0 : wet_cells >= (32ll << 20)) {
-            const int IG = p1v_group_columns(nl);
+            const int IG = p1v_group_columns(nl, d.gshift);
             std::vector<int> pos(n_owned);
             for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
             auto internal = [&](const int4 &ei) { return pos[ei.x] / IG == pos[ei.y] / IG; };
@@ -929,7 +946,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
 
 namespace {
 using PlanKey = std::tuple<const void *, const void *, const void *, const void *, const void *,
-                           const void *, const void *, int, int, int, int, int>;
+                           const void *, const void *, int, int, int, int, int, bool>;
 std::map<PlanKey, std::unique_ptr<Plan>> g_plans;
 
 template <class T>
@@ -942,12 +959,12 @@ std::vector<T> fetch(Buffer *b, size_t count)
 }  // namespace
 
 const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
-                     bool with_ring)
+                     bool with_ring, bool batched)
 {
     std::lock_guard<std::mutex> lock(g_mutex);
     PlanKey key{h.edges, h.edge_tri, h.nlev_elem, with_ring ? h.elem_nodes : nullptr,
                 with_ring ? h.nie : nullptr, with_ring ? h.nie_num : nullptr, h.nlev_nod,
-                n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0};
+                n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0, batched};
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.get();
     if (any_capture()) {  // building a plan copies with hipMemcpy, which would break an open capture
@@ -994,7 +1011,7 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
         m.dim = h.dim;
     }
     std::string err;
-    auto plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, err);
+    auto plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, plan_shape(batched), err);
     if (!plan) {
         report("invalid mesh: %s", err.c_str());
         return nullptr;

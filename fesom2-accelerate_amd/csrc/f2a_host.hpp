@@ -124,6 +124,18 @@ bool run(const char *name, hipStream_t s, F &&f)
     return good;
 }
 
+// The caller's stream waits for the overlapped halo exchange (event `done`).  With timing on, the
+// wait itself is timed as "halo_wait": from the stream reaching it (its interior work done) to the
+// exchange's completion, i.e. the part of the exchange the interior work did not hide.
+inline bool wait_halo(hipStream_t st, hipEvent_t done)
+{
+    void *tok = nullptr;
+    if (timing_enabled("halo_wait") && !capturing(st)) timing_begin("halo_wait", st, &tok);
+    const bool good = ok(hipStreamWaitEvent(st, done, 0), "hipStreamWaitEvent(halo)");
+    if (tok) timing_end(tok, st);
+    return good;
+}
+
 // ---- device allocations owned by a plan (freed with it)
 struct DeviceArrays {
     std::vector<void *> ptrs;
@@ -157,19 +169,34 @@ struct Plan {
     int lmax_edges = 0;
 };
 
+// Processing-order options of a plan.  Single-tracer calls use the defaults (16384-node patches
+// for a numbering with locality, the natural block size); calls with ntracers > 1 get a plan of
+// their own (get_plan(..., batched)): 1024-node patches and half-size blocks, because a batch's
+// tiles run (column group, tracer) tracer-fastest, which puts a column's reuse by the next row of
+// the patch ntracers times more tiles later -- beyond the XCD L2's lifetime with wide patches
+// (batched plan).
+struct PlanShape {
+    int patch = 0;   // nodes per BFS patch; 0: automatic (16384 / 4096 by numbering); 1: index order
+    int gshift = 0;  // MeshPlanDev::gshift
+};
+// the shape of the single-tracer (batched = false) or the batched plan, with the plan options
+// FESOM2_PATCH / FESOM2_BATCH_PATCH and FESOM2_BATCH_GROUP_SHIFT (read when the plan is built)
+PlanShape plan_shape(bool batched);
+
 // Node->edge CSR for nodes [0, n_csr) in ascending edge order; clusters for [0, n_owned) when the
 // element connectivity is present.  Validates every index; returns nullptr with `err` set.
 std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
-                                 int n_csr, int nl, std::string &err);
+                                 int n_csr, int nl, const PlanShape &shape, std::string &err);
 
 struct MeshHandles {
     Buffer *edges = nullptr, *edge_tri = nullptr, *nlev_elem = nullptr, *nlev_nod = nullptr;
     Buffer *elem_nodes = nullptr, *nie = nullptr, *nie_num = nullptr;
     int dim = 0;
 };
-// Cached per (handles, partition sizes); built synchronously on first use.
+// Cached per (handles, partition sizes, batched); built synchronously on first use.  `batched`: the
+// plan of calls with ntracers > 1 (PlanShape).
 const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
-                     bool with_ring);
+                     bool with_ring, bool batched = false);
 void drop_plans_of(const Buffer *b);
 // Phase marks (Buffer::int_plan) -- part of phase 2 already done by a phase-1 launch: on fct_adf_h
 // the block-internal edges of `plan` limited by p1v (fct_ale_pre_comm_v_acc_, or fct_ale_pre_comm_acc_

@@ -111,6 +111,9 @@ static_assert(sizeof(NodeRec) == 192, "NodeRec layout");
 // Device-side view of the derived mesh structures of one (mesh, partition) pair.
 struct MeshPlanDev {
     int n_owned = 0;       // myDim_nod2D
+    // block size of the column-group kernels: 2^gshift times group_columns' natural G (the batched
+    // plan halves it, see get_plan)
+    int gshift = 0;
     int n_total = 0;       // myDim_nod2D + eDim_nod2D
     int n_edges = 0;       // myDim_edge2D
     int nl = 0;
@@ -188,8 +191,9 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // phase 1 + b3v (+ the block-internal edges' b3h), no cv: fct_ale_pre_comm_acc_ in the reference
 // sequence's fast mode (no area/hnode/hnode_new/del_v needed)
 hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
-// columns per p1v block for nl levels at vlimit 1 (the shape launch_p1v uses; the plan's int_G)
-int p1v_group_columns(int nl);
+// columns per p1v block for nl levels (the shape launch_p1v uses; the plan's int_G) at the plan's
+// group shift
+int p1v_group_columns(int nl, int shift);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);
 constexpr int kMaxInternal = 64;  // most block-internal edges a p1v block limits (LDS staging)
@@ -248,8 +252,9 @@ struct P2IterArgs {
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s);
 hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
                            real *adf_h2, const Tracers &tr, hipStream_t s);
-// columns per wave for a column length L (G*L fills whole wave64 iterations where possible)
-int group_columns(int L);
+// columns per block for S slots per column (G*S fills whole wave64 iterations where possible),
+// times 2^shift
+int group_columns(int S, int shift = 0);
 
 // Stepwise kernels, one per reference step.
 hipError_t launch_a1(int n_nodes, int nl, const int *nlev_nod, const real *LO, const real *ttf,

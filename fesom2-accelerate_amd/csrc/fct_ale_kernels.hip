@@ -1094,8 +1094,10 @@ __global__ __launch_bounds__(1024) void k_b3h_iter(const int4 *__restrict__ einf
     stv_s<C, true>(adf_h + i, h2, C);
 }
 
-// columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads)
-int group_columns(int S)
+// columns per block for S slots per column: G*S fills whole waves where possible (<= 1024 threads),
+// times 2^shift (the plan's MeshPlanDev::gshift: shift < 0 halves the block; results do not depend
+// on it)
+int group_columns(int S, int shift)
 {
     int best = 1;
     double best_waste = 1e30;
@@ -1107,9 +1109,6 @@ int group_columns(int S)
         }
         if (waste < 1.0 + 1e-9) break;
     }
-    // FESOM2_GROUP_SHIFT = k (tuning build): 2^k times as many columns per block (k < 0: fewer;
-    // A/B measurements, results do not depend on it)
-    static const int shift = knob("FESOM2_GROUP_SHIFT", 0);
     for (int k = 0; k < shift && best * 2 * S <= 1024; k++) best *= 2;
     for (int k = 0; k > shift && best > 1; k--) best /= 2;
     return best;
@@ -1274,12 +1273,12 @@ static hipError_t p1_launch_tuning(const MeshPlanDev &mp, const P1Args &a, hipSt
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     if (odd_pairs(a.nl - 1) && a.vlimit == 1) {
-        const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S);
+        const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, false, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
     }
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
 #if F2A_TUNING
     // other gather batches (FESOM2_P1_BATCH = 10*RB + EB), cache policies
@@ -1305,25 +1304,18 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 #endif
 }
 
-int p1v_group_columns(int nl)
+int p1v_group_columns(int nl, int shift)
 {
     const int L = nl - 1;
-    if (odd_pairs(L)) return group_columns((L + 1) / 2);
-    return group_columns(L / levels_per_thread(L));
-}
-
-// columns per block of launch_p1v's shape for this vlimit (odd L in level pairs at vlimit 1 only)
-static int p1v_launch_G(int nl, int vlimit)
-{
-    (void)vlimit;  // every vlimit runs odd L in level pairs (round 3)
-    return p1v_group_columns(nl);
+    if (odd_pairs(L)) return group_columns((L + 1) / 2, shift);
+    return group_columns(L / levels_per_thread(L), shift);
 }
 
 // the launch_p1v forms with the internal-edge tail: the plan built the lists for this block size
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 {
     return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit >= 1 && a.vlimit <= 3 &&
-           knob("FESOM2_P1V_B3H", 1) != 0 && p1v_launch_G(a.nl, a.vlimit) == mp.int_G;
+           knob("FESOM2_P1V_B3H", 1) != 0 && p1v_group_columns(a.nl, mp.gshift) == mp.int_G;
 }
 
 
@@ -1333,7 +1325,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
 {
     const int L = a.nl - 1;
     if (odd_pairs(L) && a.vlimit != 1) {  // the product's forms (p1v_launch_G: pairs at every vlimit)
-        const int S = (L + 1) / 2, G = group_columns(S);
+        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1345,7 +1337,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
         F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
     }
     if (odd_pairs(L) && a.vlimit == 1) {
-        const int S = (L + 1) / 2, G = group_columns(S);
+        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, 1, in);
         const float inv = 1.0f / (float)S;
@@ -1358,7 +1350,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
         if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1411,7 +1403,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         const int L = a.nl - 1;
         const bool odd = odd_pairs(L);
         if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S);
+            const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
             const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
             const size_t lds = p1_lds_bytes(G, L, 1, in);
             const float inv = 1.0f / (float)S;
@@ -1435,7 +1427,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         const int L = a.nl - 1;
         const bool odd = odd_pairs(L);
         if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S);
+            const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
             const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
             const size_t lds = p1_lds_bytes(G, L, 1, in);
             const float inv = 1.0f / (float)S;
@@ -1459,7 +1451,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     // b3-horizontal, +32 their entries staged into LDS by DMA.  NT: the single-use streams
     // (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
     if (odd_pairs(L)) {  // odd L in level pairs, every vlimit (the 3-point bounds of vlimit 2/3 skip the pad level)
-        const int S = (L + 1) / 2, G = group_columns(S);
+        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1475,7 +1467,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1514,7 +1506,7 @@ hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const bool in = p1v_limits_internal(mp, a);
     const int L = a.nl - 1;
     if (odd_pairs(L)) {
-        const int S = (L + 1) / 2, G = group_columns(S);
+        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1530,7 +1522,7 @@ hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1567,7 +1559,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
     const bool pair = knob("FESOM2_NL_PAIR", 1) != 0;
     if (odd_pairs(L)) {
-        const int S = (L + 1) / 2, G = group_columns(S);
+        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
         const long groups = (long)(a.count + G - 1) / G * a.tr.n;
         const size_t lds = (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
@@ -1578,7 +1570,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 #endif
         F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1606,7 +1598,7 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     const int L = a.nl - 1;
     // levels per thread of the node kernel: FESOM2_P2_CPT (tuning build; default as the other kernels)
     const int C = (L % 2 == 0 && knob("FESOM2_P2_CPT", levels_per_thread(L)) == 2) ? 2 : 1;
-    const int S = L / C, G = group_columns(S);
+    const int S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1645,7 +1637,7 @@ hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const int L = a.nl - 1;
     const bool odd = L % 2 == 1;
     if (odd && L < 3) return hipErrorInvalidValue;
-    const int S = (L + 1) / 2, G = group_columns(S);
+    const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
     const long groups = (a.count + G - 1) / G;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1789,7 +1781,7 @@ hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus,
 
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)
 {
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1800,7 +1792,7 @@ hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_
 hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
                            real *adf_h2, const Tracers &tr, hipStream_t s)
 {
-    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S);
+    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
     const long groups = (long)(mp.n_edges + G - 1) / G * tr.n;
     const float invS = 1.0f / (float)S;
     if (C == 2)

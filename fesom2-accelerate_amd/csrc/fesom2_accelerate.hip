@@ -364,7 +364,7 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
         if (!barea || !bh || !bhn || !bdv) return;
     }
     mh.nlev_nod = bnlnod;
-    const Plan *plan = get_plan(mh, N, NT, E, NL, true);
+    const Plan *plan = get_plan(mh, N, NT, E, NL, true, ntr > 1);
     if (!plan) return;
     if (!g_resident && !h2d(blo, false, st, false)) return;
     wait_event(bttf, st);
@@ -617,7 +617,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         !mh.edges || !mh.edge_tri || !mh.nlev_elem)
         return;
     mh.nlev_nod = bnl;
-    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false, ntr > 1);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
     if (has_internal(badfh, st) || has_internal(badfv, st)) {  // part of phase 2 done already
@@ -648,7 +648,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
         if (!run("fct_ale_p2", st, [&] { return f2a::launch_p2_fused(d, a, st); })) return;
     }
     if (comm) {
-        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
+        if (!wait_halo(st, halo_done)) return;
         a.nodes = d.p2_rec + n_first;
         a.count = N - n_first;
         {
@@ -700,7 +700,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
     if (!bplus || !bminus || !badfh || !bdh || !barea || !bnl || !mh.edges || !mh.edge_tri || !mh.nlev_elem) return;
     mh.nlev_nod = bnl;
-    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false, ntr > 1);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
     // the block-internal edges p1v limited already (fct_ale_pre_comm_v_acc_ marked fct_adf_h with
@@ -737,7 +737,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
         return;
     if (!run("fct_ale_p2h", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
     if (exch) {
-        if (!ok(hipStreamWaitEvent(st, halo_done, 0), "hipStreamWaitEvent(halo)")) return;
+        if (!wait_halo(st, halo_done)) return;
         if (!run("fct_ale_b3_horizontal_boundary", st, [&] {
                 return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
                                              dptr<real>(badfh), a.tr, st);
@@ -850,7 +850,7 @@ static void post_comm_iter_impl(int *alg_state, void **s, int ntr, void **fct_pl
         !mh.edge_tri || !mh.nlev_elem)
         return;
     mh.nlev_nod = bnl;
-    const Plan *plan = get_plan(mh, N, NT, E, NL, false);
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false, ntr > 1);
     if (!plan) return;
     const f2a::MeshPlanDev &d = plan->dev;
     if (has_internal(badfh, st) || has_internal(badfv, st)) {  // part of phase 2 done already
@@ -946,7 +946,8 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
 // Diagnostics of the mesh plan the phase-1 kernels run on (for the benchmark's byte counts):
 // info[0] p1v block columns of the internal-edge lists (0: none), [1] interior edges (both
 // endpoints owned), [2] interior edges crossing p1v blocks (b3h's), [3] block-internal edges
-// (limited inside p1v), [4] their edge cells (sum of levels).  *ninfo: entries written.
+// (limited inside p1v), [4] their edge cells (sum of levels); [5, 10) the same for the plan of batched
+// calls (ntracers > 1, built here if needed).  *ninfo: entries wanted (<= 10) / written.
 void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
                        int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
                        void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
@@ -965,12 +966,14 @@ void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim
     mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
     mh.dim = *nod_in_elem2D_dim;
     if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !mh.nlev_nod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
-    const Plan *plan = get_plan(mh, N, NT, E, *nl, true);
-    if (!plan) return;
-    const long long v[5] = {plan->dev.int_G, plan->dev.n_edge_interior, plan->dev.n_ext_interior,
-                            plan->dev.n_edge_interior - plan->dev.n_ext_interior, plan->int_cells};
-    const int n = std::min(*ninfo, 5);
-    for (int k = 0; k < n; k++) info[k] = v[k];
+    const int n = std::min(*ninfo, 10);
+    for (int part = 0; part * 5 < n; part++) {  // [0, 5) the single-tracer plan, [5, 10) the batched one
+        const Plan *plan = get_plan(mh, N, NT, E, *nl, true, part == 1);
+        if (!plan) return;
+        const long long v[5] = {plan->dev.int_G, plan->dev.n_edge_interior, plan->dev.n_ext_interior,
+                                plan->dev.n_edge_interior - plan->dev.n_ext_interior, plan->int_cells};
+        for (int k = 0; k < 5 && part * 5 + k < n; k++) info[part * 5 + k] = v[k];
+    }
     *ninfo = n;
     *istat = 0;
 }

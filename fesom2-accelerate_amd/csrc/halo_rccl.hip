@@ -258,7 +258,12 @@ hipEvent_t halo_exchange_async(void **comm, void **plan, Buffer *bp, Buffer *bm,
     if (!ok(hipEventRecord(p->ev_ready, s), "hipEventRecord(halo ready)") ||
         !ok(hipStreamWaitEvent(p->cstream, p->ev_ready, 0), "hipStreamWaitEvent(halo ready)"))
         return nullptr;
-    if (!exchange_on(c, p, bp, bm, ntr, stride, p->cstream)) return nullptr;
+    // timed as "halo_exchange" (pack, grouped send/recv, unpack on the halo stream) when timing is on
+    void *tok = nullptr;
+    if (timing_enabled("halo_exchange") && !capturing(s)) timing_begin("halo_exchange", p->cstream, &tok);
+    const bool sent = exchange_on(c, p, bp, bm, ntr, stride, p->cstream);
+    if (tok) timing_end(tok, p->cstream);
+    if (!sent) return nullptr;
     if (!ok(hipEventRecord(p->ev_done, p->cstream), "hipEventRecord(halo done)")) return nullptr;
     return p->ev_done;
 }

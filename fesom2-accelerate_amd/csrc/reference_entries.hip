@@ -161,7 +161,7 @@ void fct_ale_a4_reference_(int *nNodes2D, int *nLevels_nod2D, int *nLevels_elem2
     hm.nlev_elem = nLevels_elem2D;
     hm.n_elem_total = ne;
     std::string err;
-    auto plan = build_plan(hm, (int)nn, (int)nn, (int)E, (int)nn, *nl, err);
+    auto plan = build_plan(hm, (int)nn, (int)nn, (int)E, (int)nn, *nl, PlanShape{}, err);
     if (!plan) {
         report("fct_ale_a4_reference_: invalid mesh: %s", err.c_str());
         return;

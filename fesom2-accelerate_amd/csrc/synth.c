@@ -148,3 +148,15 @@ void synth_fill(uint64_t seed, int field, int dist, int64_t ncols, int stride, c
         }
     }
 }
+
+/*
+ * Levels of elements [t0, t0 + count) of the triangulation synth_mesh_build makes with the same
+ * (nl, seed, full_depth): the strip generator of fesom2_amd/partition.py builds a rank's local mesh
+ * from these without the global mesh.
+ */
+void synth_elem_levels(int nl, uint64_t seed, int full_depth, int64_t t0, int64_t count, int *out)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < count; k++)
+        out[k] = full_depth ? nl : 3 + (int)(hash3(seed, 1, (uint64_t)(t0 + k)) % (uint64_t)(nl - 2));
+}

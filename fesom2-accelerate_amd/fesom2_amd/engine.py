@@ -53,18 +53,20 @@ class DeviceMesh:
                                    ip(m.dim), h["edges"].ref, h["edge_tri"].ref)
         check(st, "fesom2_prepare_mesh_")
 
-    def info(self):
+    def info(self, batched=False):
         """fesom2_mesh_info_: p1v block columns, interior edges, those crossing p1v blocks, the
-        block-internal ones (limited inside p1v) and their edge cells."""
+        block-internal ones (limited inside p1v) and their edge cells -- of the single-tracer plan,
+        or with ``batched`` of the plan calls with ntracers > 1 run on."""
         m, h = self.m, self.h
-        st, n = C.c_int(0), C.c_int(5)
-        out = (C.c_longlong * 5)()
+        st, n = C.c_int(0), C.c_int(10 if batched else 5)
+        out = (C.c_longlong * 10)()
         dll().fesom2_mesh_info_(C.byref(st), ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), h["nlev_nod"].ref,
                                 h["nlev_elem"].ref, h["elem2D_nodes"].ref, h["nie_num"].ref, h["nie"].ref,
                                 ip(m.dim), h["edges"].ref, h["edge_tri"].ref, out, C.byref(n))
         check(st, "fesom2_mesh_info_")
         keys = ("p1v_columns", "interior_edges", "crossing_edges", "internal_edges", "internal_edge_cells")
-        return dict(zip(keys, list(out)[: n.value]))
+        vals = list(out)[: n.value]
+        return dict(zip(keys, vals[5:] if batched else vals))
 
     def free(self):
         for h in self.h.values():
@@ -265,16 +267,37 @@ class FctAle:
     # ------------------------------------------------------------------ data movement
     def upload(self, name, a=None):
         a = self.host[name] if a is None else np.ascontiguousarray(a, dtype=np.float64)
+        if a.size < self.size(name):
+            raise ValueError(f"upload {name}: {a.size} doubles for a handle of {self.size(name)}")
         st = C.c_int(0)
         dll().fesom2_upload_(self.h[name].ref, arr(a), C.byref(st))
         check(st, f"upload {name}")
 
-    def download(self, name, dtype=np.float64):
+    def size(self, name):
+        """Doubles the handle of ``name`` holds (its host array's size; kept by drop_host)."""
+        sizes = getattr(self, "sizes", {})
+        if name in sizes:
+            return sizes[name]
+        if name in self.host:
+            return self.host[name].size
+        return {"UV_rhs": 2 * self.m.L * self.m.T}.get(name, (self.m.N + self.m.H) * self.m.L)
+
+    def drop_host(self):
+        """Release the host copies of the fields (device-resident runs on large meshes): downloads
+        keep working (sizes are kept), uploads then need an explicit array.  The library never reads
+        the bound host pointers in resident mode (fesom2_set_resident_(1))."""
+        self.sizes = {k: v.size for k, v in self.host.items()}
+        self.host = {}
+
+    def download(self, name, dtype=np.float64, out=None):
+        """The handle's contents; into ``out`` (float64, contiguous, at least max(n, 1) doubles:
+        e.g. a memory-mapped file) when given."""
         b = self.h[name]
-        n = {"UV_rhs": 2 * self.m.L * self.m.T}.get(name, self.host[name].size if name in self.host else None)
-        if n is None:
-            n = (self.m.N + self.m.H) * self.m.L
-        out = np.empty(max(n, 1), dtype)  # every handle here holds exactly max(n, 1) doubles
+        n = self.size(name)
+        if out is None:
+            out = np.empty(max(n, 1), dtype)  # every handle here holds exactly max(n, 1) doubles
+        elif out.dtype != np.float64 or not out.flags.c_contiguous or out.size < max(n, 1):
+            raise ValueError(f"download {name}: output buffer does not fit {max(n, 1)} doubles")
         st = C.c_int(0)
         dll().fesom2_download_(b.ref, arr(out), C.byref(st))
         check(st, f"download {name}")

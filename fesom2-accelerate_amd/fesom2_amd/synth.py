@@ -201,28 +201,40 @@ def fill(seed, field, dist, ncols, stride, gid, a, b):
     return out
 
 
+FIELDS = ("ttf", "LO", "adf_v", "adf_h", "area", "area_inv", "hnode", "hnode_new", "del_v", "del_h")
+
+
+def make_field(m: Mesh, name, seed=43, area_scale=1.0, adf_scale=0.5):
+    """One field of :func:`make_fields` (the same bits): bench.py regenerates the pristine inputs of
+    its parity check field by field instead of keeping a second host copy of a 9.6M-node mesh."""
+    NT, L, nl = m.N + m.H, m.L, m.nl
+    g = m.node_gid
+    if name in ("ttf", "LO", "del_v", "del_h"):
+        return fill(seed, name, 1, NT, L, g, 0.0, 1.0)
+    if name == "adf_v":
+        adf_v = fill(seed, "adf_v", 1, NT, nl, g, 0.0, adf_scale).reshape(NT, nl)
+        # the bottom flux is always zero (docs/refactoring.md:232)
+        adf_v[np.arange(nl)[None, :] >= (m.nlev_nod[:, None] - 1)] = 0.0
+        return adf_v.reshape(-1)
+    if name == "adf_h":
+        return fill(seed, "adf_h", 1, m.E, L, m.edge_gid, 0.0, adf_scale)
+    if name == "area":
+        return fill(seed, "area", 0, NT, nl, g, 0.5 * area_scale, 2.0 * area_scale)
+    if name == "area_inv":
+        return 1.0 / make_field(m, "area", seed, area_scale, adf_scale)
+    if name in ("hnode", "hnode_new"):
+        return fill(seed, name, 0, NT, L, g, 5.0, 50.0)
+    raise KeyError(name)
+
+
 def make_fields(m: Mesh, seed=43, area_scale=1.0, adf_scale=0.5):
     """All per-tracer and per-mesh fields of one pass, keyed on global ids.
 
     Scales keep the limiter active (ratios in b2 of order one) so b2/b3 are exercised.
     """
-    NT, L, nl = m.N + m.H, m.L, m.nl
-    g = m.node_gid
-    f = {}
-    f["ttf"] = fill(seed, "ttf", 1, NT, L, g, 0.0, 1.0)
-    f["LO"] = fill(seed, "LO", 1, NT, L, g, 0.0, 1.0)
-    adf_v = fill(seed, "adf_v", 1, NT, nl, g, 0.0, adf_scale).reshape(NT, nl)
-    # the bottom flux is always zero (docs/refactoring.md:232)
-    adf_v[np.arange(nl)[None, :] >= (m.nlev_nod[:, None] - 1)] = 0.0
-    f["adf_v"] = adf_v.reshape(-1)
-    f["adf_h"] = fill(seed, "adf_h", 1, m.E, L, m.edge_gid, 0.0, adf_scale)
-    f["area"] = fill(seed, "area", 0, NT, nl, g, 0.5 * area_scale, 2.0 * area_scale)
+    f = {k: make_field(m, k, seed, area_scale, adf_scale) for k in FIELDS if k != "area_inv"}
     f["area_inv"] = 1.0 / f["area"]
-    f["hnode"] = fill(seed, "hnode", 0, NT, L, g, 5.0, 50.0)
-    f["hnode_new"] = fill(seed, "hnode_new", 0, NT, L, g, 5.0, 50.0)
-    f["del_v"] = fill(seed, "del_v", 1, NT, L, g, 0.0, 1.0)
-    f["del_h"] = fill(seed, "del_h", 1, NT, L, g, 0.0, 1.0)
-    return f
+    return {k: f[k] for k in FIELDS}
 
 
 def make_tracer_fields(m: Mesh, ntracers, seed=43, **kw):

@@ -144,16 +144,19 @@ void fesom2_set_resident_(int *resident);
  * then only moves fct_adf_v, fct_ale_post_comm_acc_ limits the remaining edges.  Same results;
  * phase-2 entries other than inter_comm/post_comm refuse fct_adf_v/fct_adf_h touched this way. */
 void fesom2_set_path_(int *path);
-/* Build the derived mesh structures (edge/ring CSR) ahead of the first pass (otherwise built
- * lazily, synchronously, on first use). */
+/* Build the derived mesh structures (edge/ring CSR, processing order) ahead of the first pass
+ * (otherwise built lazily, synchronously, on first use).  Calls with ntracers > 1 run on a plan of
+ * their own (smaller patches and blocks for the batch's tile order), built on the first such call
+ * or by fesom2_mesh_info_ with *ninfo >= 10. */
 void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D,
                           int *myDim_edge2D, int *nl, void **nlevels_nod2D, void **nlevels_elem2D,
                           void **elem2D_nodes, void **nod_in_elem2D_num, void **nod_in_elem2D,
                           int *nod_in_elem2D_dim, void **nod2D_edges, void **elem2D_edges);
 /* Diagnostics of the phase-1 mesh plan (built if needed): info[0] p1v block columns of the
  * block-internal edge lists (0 = none), [1] interior edges, [2] interior edges crossing p1v blocks,
- * [3] block-internal edges (limited inside fct_ale_pre_comm_v_acc_), [4] their edge cells.
- * *ninfo: capacity in, entries written out. */
+ * [3] block-internal edges (limited inside fct_ale_pre_comm_v_acc_), [4] their edge cells;
+ * [5, 10) the same for the plan of batched calls (ntracers > 1).  *ninfo: capacity in (at most 10
+ * used), entries written out. */
 void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
                        int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
                        void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,

@@ -73,12 +73,13 @@ def test_mode_switches_do_not_need_a_device():
 def test_product_library_reads_only_the_plan_options():
     """The product library has no A/B knobs: the only environment variables it names are the plan
     options read when a mesh plan is built, and none of the measured-and-rejected
-    variants (fct_ale_variants.hip: k_p2w, k_p2f, k_p1e, k_p1s, k_p2hf, k_b3h_n) is in it."""
+    variants deleted in round 4 (k_p2w, k_p2f, k_p1e, k_p1s, k_p2hf, k_b3h_n, k_p1p, k_p1t) is in it."""
     data = open(LIB, "rb").read()
     names = set(re.findall(rb"FESOM2_[A-Z0-9_]+", data))
-    assert names <= {b"FESOM2_PATH", b"FESOM2_NUM_KERNELS", b"FESOM2_P1V_B3H", b"FESOM2_PATCH"}, names
+    assert names <= {b"FESOM2_PATH", b"FESOM2_NUM_KERNELS", b"FESOM2_P1V_B3H", b"FESOM2_PATCH",
+                     b"FESOM2_BATCH_PATCH", b"FESOM2_BATCH_GROUP_SHIFT"}, names
     syms = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True, check=True).stdout
-    for k in ("k_p2w", "k_p2f", "k_p1e", "k_p1s", "k_p2hf", "k_b3h_n", "launch_p1_variant"):
+    for k in ("k_p2w", "k_p2f", "k_p1e", "k_p1s", "k_p2hf", "k_b3h_n", "k_p1p", "k_p1t", "launch_p1_variant"):
         assert not re.search(rf"\b{k}\b", syms), k
 
 

@@ -242,3 +242,42 @@ def test_split_by_direction_partitioned_overlap(comm, internal, nl, monkeypatch)
         for name, w in (("del_v", L), ("del_h", L), ("adf_v", nl)):
             got = partition.gather_owned(ms, lambda r: outs[r][name].reshape(ntr, -1)[k], w, g.N)
             assert np.array_equal(got, wants[k][name]), (name, k)
+
+
+@pytest.mark.parametrize("shape", [{}, {"FESOM2_BATCH_GROUP_SHIFT": "0"},
+                                   {"FESOM2_BATCH_GROUP_SHIFT": "-2", "FESOM2_BATCH_PATCH": "64"},
+                                   {"FESOM2_BATCH_PATCH": "1"}],
+                         ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()) or "default")
+@pytest.mark.parametrize("name,full", [("8k x 20", False), ("127k x 47", True)])
+@pytest.mark.parametrize("internal", ["0", "1"])
+def test_batched_plan_shapes(shape, name, full, internal, monkeypatch):
+    """Batched calls run on a plan of their own (smaller patches, half-size blocks by default: the
+    plan options FESOM2_BATCH_PATCH / FESOM2_BATCH_GROUP_SHIFT); the single-tracer plan is unchanged.
+    Every shape is exact on every tracer, with and without the block-internal edges in p1v (whose
+    lists follow the batched plan's block size)."""
+    for k, v in dict(shape, FESOM2_P1V_B3H=internal).items():
+        monkeypatch.setenv(k, v)
+    m = synth.config_mesh(name, full_depth=full)
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        one, many = dm.info(), dm.info(batched=True)
+        if internal == "1" and many["p1v_columns"]:  # (0: some block has too many internal edges)
+            shift = int(shape.get("FESOM2_BATCH_GROUP_SHIFT", "-1"))
+            assert many["p1v_columns"] * 2 ** -shift == one["p1v_columns"], (one, many)
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        for k in range(3):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+        # the fused batched pair on the same plan
+        for name_ in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(name_)
+        assert e.full_pass() == 9, abi.last_error()
+        e.sync()
+        for k in range(3):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+    finally:
+        e.free()
+        dm.free()

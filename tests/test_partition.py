@@ -159,3 +159,27 @@ def test_gloo_two_ranks_matches_single_domain():
         for k, v in owned.items():
             assert np.array_equal(v, want[k].reshape(-1, L)[gid]), (rank, k)
     assert seen.all()
+
+
+@pytest.mark.parametrize("nx,ny,nl,world,full", [(8, 6, 7, 2, False), (16, 9, 9, 3, False), (24, 16, 11, 4, True),
+                                                 (5, 7, 6, 7, False), (10, 4, 5, 1, False), (12, 10, 9, 5, False)])
+def test_strip_local_mesh_equals_the_cut_of_the_global_mesh(nx, ny, nl, world, full):
+    """partition.strip_local_mesh builds a rank's y-strip from closed formulas of the structured
+    numbering (no global mesh: what a rank of the 9.6M-node bench and the parallel check workers use);
+    every array, count and exchange list equals local_mesh's cut of synth.make_mesh."""
+    g = synth.make_mesh(nx, ny, nl, full_depth=full)
+    parts = partition.strip_parts(nx, ny, world)
+    row_part = parts.reshape(ny, nx)[:, 0]
+    for r in range(world):
+        y0, y1 = partition.strip_rows(ny, world, r)
+        a, ha = partition.local_mesh(g, parts, r)
+        b, hb = partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=full, row_part=row_part, rank=r)
+        for f in ("nl", "N", "H", "T", "E", "dim"):
+            assert getattr(a, f) == getattr(b, f), (f, r)
+        for f in ("elem2D_nodes", "edges", "edge_tri", "nie_num", "nie", "nlev_elem", "nlev_nod", "node_gid",
+                  "edge_gid"):
+            x, y = getattr(a, f), getattr(b, f)
+            assert x.dtype == y.dtype and np.array_equal(x, y), (f, r)
+        assert ha.neighbors == hb.neighbors
+        for q in ha.neighbors:
+            assert np.array_equal(ha.send[q], hb.send[q]) and np.array_equal(ha.recv[q], hb.recv[q]), (r, q)
