@@ -19,13 +19,25 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 * value     cell-updates/s = (sum over ranks of owned wet cells N_owned x L) / (max-over-ranks time per step).
 * roofline  the dominant kernel's algorithmic bytes per launch / its average launch time (HIP events
             on its stream, recorded inside the library around each of its launches in the timed region;
-            the other kernels are timed on up to 10 extra steps after it), against 8.0 TB/s.
-* check     one more pass on pristine inputs, compared cell for cell with the oracle (per rank on its
-            local mesh at N > 1); a mismatch exits with status 1.
+            the other kernels are timed on up to 10 extra steps after it), against 8.0 TB/s; both byte
+            models: the kernel's own (alg_bytes_per_launch -> frac) and SURVEY.md 8(d)'s strict
+            minimum for the same work (alg_bytes_min -> frac_min).
+* check     one more pass on pristine inputs, compared cell for cell with the oracle: on structured
+            meshes by a pool of worker processes (spawned before the GPU is touched), each running
+            the oracle on a row strip of the rank's domain widened by one ring (exact without any
+            exchange); a mismatch exits with status 1.
+* extra     (default --extras auto) further BASELINE configs in the same run, each with its own
+            timing, roofline and check: at N = 1 configs[1] (127k x 47, 1 and 6 tracers), configs[3]
+            (1.2M x 80, 6 tracers batched) and configs[4]'s strong-scaling base (9.6M x 80 on one
+            GPU); at N > 1 the strong-scaling leg (9.6M x 80 split over the N GPUs).  Every N > 1
+            record carries the per-rank spread of step times and the halo exchange's own time and
+            hidden fraction.
 * cpu_baseline  the oracle's single-threaded full pass (bit-identical to reference.cpp for a1..b2)
             on the same mesh, rank 0 at N = 1 only; plus "all_cores": P single-threaded oracle
             processes on a P-way strip partition of the same mesh (MPI-style replicas, SURVEY.md
             8(d)), run before this process touches the GPU.
+* watchdog  a thread per rank: RCCL communicator setup, the first exchange step and each leg have a
+            time bound; past it the rank prints its stage to stderr and exits (os._exit, status 3).
 
 Loads the engine library before torch so the process runs on one HIP runtime; torch is used only
 for the multi-rank control plane (gloo: barrier, max-reduce, RCCL unique-id broadcast).
@@ -33,10 +45,13 @@ for the multi-rank control plane (gloo: barrier, max-reduce, RCCL unique-id broa
 from __future__ import annotations
 
 import argparse
+import copy
 import ctypes as C
+import gc
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -48,6 +63,7 @@ from fesom2_amd import abi, engine, partition, synth  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
 METRIC = "FCT-ALE cell-updates/sec (nodes×levels) at 1/2/4/8 GPUs; % HBM roofline"
+OUTPUTS = (("plus", "L"), ("minus", "L"), ("del_v", "L"), ("del_h", "L"), ("adf_v", "nl"), ("adf_h", "L"))
 
 
 def log(*a):
@@ -92,16 +108,10 @@ def kernel_bytes(s, ntr=1, split=False):
     # p2: plus, minus, adf_v (r + w), del_v (r + w), del_h (r + w), ttf, LO, adf_h; area, hnode,
     # hnode_new shared
     p2 = ntr * 8 * (9 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
-    # p2 with b3h folded in: p2 + the limited adf_h written once (the other endpoint's plus/minus
-    # columns are re-reads of arrays p2 already reads)
-    p2f = p2 + ntr * 8 * ce
     # split by direction: phase 1 + b3v/cv (adds the limited adf_v write, del_v rw; hnode, hnode_new,
     # area shared), then c-horizontal alone (del_h rw, adf_h; area shared)
     p1v = p1 + ntr * 8 * (cn + 2 * cn + ice) + 8 * 3 * cn + 16 * nie
     p2h = ntr * 8 * (2 * cn + ce) + 8 * cn + 4 * N + ints_edges
-    # c-horizontal with b3h folded in: raw adf_h read, limited adf_h written once, plus/minus of both
-    # endpoints (owned + halo columns), del_h rw; area shared
-    p2hf = ntr * 8 * (2 * cn + 2 * ce + 2 * (cn + ch)) + 8 * cn + 4 * N + ints_edges + 4 * E
     # reference entry sequence in the fast mode: phase 1 + b3v (+ the internal edges) in one kernel
     p1b3v = p1 + ntr * 8 * (cn + ice) + 16 * nie
     # reference entry sequence on the fused kernels: b3v alone (plus/minus, adf_v rw) and the c-step
@@ -109,10 +119,33 @@ def kernel_bytes(s, ntr=1, split=False):
     b3v = ntr * 8 * (2 * cn + 2 * cn1) + 4 * N
     c_step = ntr * 8 * (4 * cn + 2 * cn + cn1 + ce) + 8 * 3 * cn + 4 * N + ints_edges
     survey = 32 * cn + ntr * (120 * cn + 24 * ce)  # SURVEY.md §8(d), ints not counted (= 152 Cn + 24 Ce at 1)
-    return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2, "fct_ale_p2_b3h": p2f,
-            "fct_ale_p1v": p1v, "fct_ale_p2h": p2h, "fct_ale_p2h_b3h": p2hf,
+    return {"fct_ale_p1": p1, "fct_ale_b3_horizontal": b3h, "fct_ale_p2": p2,
+            "fct_ale_p1v": p1v, "fct_ale_p2h": p2h,
             "fct_ale_b3_vertical": b3v, "fct_ale_c": c_step, "fct_ale_p1_b3v": p1b3v,
-            "pass": p1 + b3h + p2, "pass_fused": p1 + p2f, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
+            "pass": p1 + b3h + p2, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
+
+
+def kernel_bytes_min(s, ntr=1):
+    """SURVEY.md 8(d)'s strict minimum bytes for the work of the phase-1 kernels (each array of its
+    table read or written once, no index arrays, no halo columns, no internal-edge flux writes):
+    phase 1 = ttf, LO, adf_v, area_inv read + plus/minus written = 48 Cn, + adf_h read 8 Ce; p1v
+    adds the vertical half of phase 2 (limited adf_v written, del_v read + written, hnode,
+    hnode_new, area read) = 48 Cn.  Mesh fields (area_inv; area, hnode, hnode_new) count once per
+    batch: p1 = 8 Cn + ntr (40 Cn + 8 Ce), p1v = 32 Cn + ntr (64 Cn + 8 Ce) (96 Cn + 8 Ce at 1)."""
+    cn, ce = s["cn"], s["ce"]
+    return {"fct_ale_p1": 8 * cn + ntr * (40 * cn + 8 * ce),
+            "fct_ale_p1v": 32 * cn + ntr * (64 * cn + 8 * ce)}
+
+
+# ----------------------------------------------------------------------------- worker pool
+
+def make_pool(world):
+    """Worker processes for the CPU baselines and the parity check, spawned before this process
+    touches the GPU (they never do): min(16, usable cores / ranks) per rank -- 16 is the GPU box's
+    CPU share per GPU."""
+    import multiprocessing
+    P = max(1, min(16, len(os.sched_getaffinity(0)) // max(world, 1)))
+    return multiprocessing.get_context("spawn").Pool(P), P
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -123,22 +156,17 @@ def _cpu_replica(job):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     nx, ny, nl = synth.CONFIGS[config]
-    g = synth.make_mesh(nx, ny, nl, full_depth=full_depth)
-    m, _ = partition.local_mesh(g, partition.strip_parts(nx, ny, P), p)
-    del g
+    y0, y1 = partition.strip_rows(ny, P, p)
+    m, _ = partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=full_depth)
     best, reps = O.time_full_pass(m, synth.make_fields(m), budget_s=budget)
     return int((m.nlev_nod[: m.N].astype(np.int64) - 1).sum()), best, reps
 
 
-def cpu_all_cores(args, budget=4.0):
+def cpu_all_cores(args, pool, P, budget=4.0):
     """P concurrent single-threaded oracle processes on a P-way partition of the workload mesh;
-    value = all owned cells / the slowest replica's best pass.  P = the cores this process may use,
-    at most 16 (the GPU box's CPU share per GPU)."""
-    import multiprocessing
-    P = max(1, min(16, len(os.sched_getaffinity(0))))
+    value = all owned cells / the slowest replica's best pass."""
     jobs = [(args.config, not args.parity_levels, P, p, budget) for p in range(P)]
-    with multiprocessing.get_context("spawn").Pool(P) as pool:
-        res = pool.map(_cpu_replica, jobs)
+    res = pool.map(_cpu_replica, jobs)
     cells = sum(r[0] for r in res)
     slowest = max(r[1] for r in res)
     return {"value": round(cells / slowest, 1), "unit": "cell-updates/s", "cores": P,
@@ -174,6 +202,45 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
+# ----------------------------------------------------------------------------- watchdog
+
+class Watchdog:
+    """Bounds the stages that can stall a multi-rank run without a diagnosis (RCCL communicator
+    setup, the first exchange, a whole leg): past the bound the rank prints its stage and exits
+    with status 3 (os._exit: no re-exec, no cleanup that could block on the stalled collective).
+    ``on_fire`` (rank 0) may print what was measured so far first."""
+
+    def __init__(self, rank):
+        self.rank, self.stage, self.deadline, self.bound = rank, None, None, 0.0
+        self.on_fire = None
+        self.lock = threading.Lock()
+        threading.Thread(target=self._loop, daemon=True, name="bench-watchdog").start()
+
+    def arm(self, stage, seconds):
+        with self.lock:
+            self.stage, self.bound, self.deadline = stage, seconds, time.monotonic() + seconds
+
+    def disarm(self):
+        with self.lock:
+            self.stage = self.deadline = None
+
+    def _loop(self):
+        while True:
+            time.sleep(0.5)
+            with self.lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                stage, bound = self.stage, self.bound
+            if late:
+                log(f"rank {self.rank}: watchdog: stage '{stage}' not done within {bound:.0f} s -- exiting")
+                try:
+                    if self.on_fire:
+                        self.on_fire(stage)
+                finally:
+                    sys.stderr.flush()
+                    sys.stdout.flush()
+                    os._exit(3)
+
+
 # ----------------------------------------------------------------------------- workload
 
 def global_dims(args, world):
@@ -189,25 +256,30 @@ def delaunay(args, npts, nl):
 
 
 def build_local(args, rank, world):
+    """This rank's local mesh (owned y-strip + one-ring halo, built from the strip alone:
+    partition.strip_local_mesh) and its exchange lists."""
     nx, ny, nl = global_dims(args, world)
     if args.mesh != "structured":
         if world > 1:
             raise SystemExit("--mesh delaunay* is a single-GPU variant")
         return delaunay(args, nx * ny, nl), None
-    g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels, name=f"{args.config} x {world}")
+    name = f"{args.config} x {world}" if args.scaling == "weak" else f"{args.config} / {world}"
     if world == 1:
+        g = synth.make_mesh(nx, ny, nl, full_depth=not args.parity_levels, name=name)
         return (synth.permute_mesh(g) if args.permuted else g), None
     if args.permuted:
         raise SystemExit("--permuted is a single-GPU stress variant")
-    part = partition.strip_parts(nx, ny, world)
-    return partition.local_mesh(g, part, rank)  # (local mesh, halo lists)
+    y0, y1 = partition.strip_rows(ny, world, rank)
+    row_part = (np.arange(ny) * world) // ny
+    return partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=not args.parity_levels, row_part=row_part,
+                                      rank=rank, name=f"{name}[rank {rank}]")
 
 
 def host_halo_exchange(dist, lists, cols):
     """FESOM's exchange_nod over gloo for (NT, L) host arrays ``cols`` (owned columns to each
     neighbour, its columns into our halo), in place.  Used by bench's --exchange host step and by the
-    per-rank oracle of the parity check (the same exchange test_partition.py checks against the
-    single-domain pass)."""
+    per-rank oracle of the serial parity check (the same exchange test_partition.py checks against
+    the single-domain pass)."""
     import torch
     ops, bufs = [], {}
     for q in lists.neighbors:
@@ -245,13 +317,25 @@ def oracle_local(m, fields, args, dist=None, lists=None):
     return out
 
 
+def _compare(bad, name, a, b, acc):
+    """Count differing cells of a vs b into bad[name]; acc = [max_abs, cells]."""
+    diff = a != b
+    n = int(np.count_nonzero(diff))
+    acc[1] += a.size
+    if n:
+        bad[name] = bad.get(name, 0) + n
+        with np.errstate(invalid="ignore"):
+            d = np.abs(a[diff] - b[diff])
+        acc[0] = max(acc[0], float(np.nanmax(d)) if np.isfinite(d).any() else float("inf"))
+
+
 def compare_local(m, got, want):
     """Cell-for-cell comparison of one rank's results with its oracle: plus/minus on the owned wet
     cells, del_v/del_h/fct_adf_v on every owned cell, fct_adf_h on every local edge.  Returns
     (mismatch counts per field, max |got - want|, cells compared)."""
     L, nl = m.L, m.nl
     wet = np.arange(L)[None, :] < (m.nlev_nod[: m.N, None].astype(np.int64) - 1)
-    bad, max_abs, cells = {}, 0.0, 0
+    bad, acc = {}, [0.0, 0]
     for k, w in enumerate(want):
         for name, width, rows, mask in (("plus", L, m.N, wet), ("minus", L, m.N, wet), ("del_v", L, m.N, None),
                                         ("del_h", L, m.N, None), ("adf_v", nl, m.N, None),
@@ -260,47 +344,158 @@ def compare_local(m, got, want):
             b = w[name][: rows * width].reshape(rows, width)
             if mask is not None:
                 a, b = a[mask], b[mask]
-            diff = a != b
-            n = int(np.count_nonzero(diff))
-            cells += a.size
-            if n:
-                bad[name] = bad.get(name, 0) + n
-                with np.errstate(invalid="ignore"):
-                    d = np.abs(a[diff] - b[diff])
-                max_abs = max(max_abs, float(np.nanmax(d)) if np.isfinite(d).any() else float("inf"))
-    return bad, max_abs, cells
+            _compare(bad, name, a, b, acc)
+    return bad, acc[0], acc[1]
 
 
-def verify(args, e, step, m, fields, world, dist, lists, want=None):
-    """The reference harness's verify-before-report (kernels/fct_ale_b2.py:97-100, ``answer=``):
-    one pass on the pristine inputs, then every rank compares its owned cells (and local edges) with
-    the oracle run on its own local mesh -- in parallel on all ranks, the plus/minus halo exchanged
-    over gloo for the oracle -- and the counts are summed over ranks.  ``want``: the oracle's outputs
-    already computed for cpu_baseline (1 tracer, N = 1)."""
+def _check_strip(job):
+    """Parallel parity check, one worker job: the oracle on rows [a, b) of rank rows [R0, R1) of the
+    structured nx x ny mesh, compared with the rank's GPU outputs (memory-mapped files).
+
+    The oracle runs on the strip widened by one row on each side as owned nodes (plus their
+    one-ring halo): every node of rows [a-1, b] then has its whole cluster and all of its edges, so
+    its plus/minus are final without an exchange, and so are the b3-limited fluxes and the c-step of
+    rows [a, b).  Node sums keep the global edge order, hence the comparison is cell-for-cell exact.
+    Edges are compared by the strip of their smallest rank-owned endpoint (each local edge once)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nx, ny, nl, full, vlimit, (R0, R1), (a, b), ntr, files = job
+    L = nl - 1
+    y0, y1 = max(0, a - 1), min(ny, b + 1)
+    m, _ = partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=full)
+    n0, n1 = (a - y0) * nx, (b - y0) * nx        # rows [a, b) in the widened strip
+    g0 = (a - R0) * nx                           # ... and in the rank's owned numbering
+    ends = m.node_gid[m.edges.reshape(-1, 2) - 1]
+    owned = (ends >= R0 * nx) & (ends < R1 * nx)
+    key = np.where(owned, ends, np.iinfo(np.int64).max).min(axis=1)
+    tgt = (key >= a * nx) & (key < b * nx)
+    gpu_e = partition.strip_edge_index(nx, ny, R0, R1, m.edge_gid[tgt])
+    wet = np.arange(L)[None, :] < (m.nlev_nod[n0:n1, None].astype(np.int64) - 1)
+    mm = {k: np.memmap(path, dtype=np.float64, mode="r", shape=shape) for k, (path, shape) in files.items()}
+    bad, acc = {}, [0.0, 0]
+    for k in range(ntr):
+        f = synth.make_fields(m, seed=43 + k)
+        if k:  # one ocean state: the mesh fields of every tracer are the first one's (make_tracer_fields)
+            f0 = synth.make_fields(m, seed=43)
+            for name in ("area", "area_inv", "hnode", "hnode_new"):
+                f[name] = f0[name]
+        st, p1 = O.pre_comm(m, f, vlimit=vlimit)
+        if st != 5:
+            raise RuntimeError(f"oracle pre_comm stopped at alg_state {st}")
+        w = O.post_comm(m, f, p1["plus"], p1["minus"])
+        w.update(plus=p1["plus"], minus=p1["minus"])
+        for name, width in OUTPUTS:
+            wd = L if width == "L" else nl
+            got = mm[name][k]
+            if name == "adf_h":
+                _compare(bad, name, got.reshape(-1, wd)[gpu_e], w[name].reshape(-1, wd)[tgt], acc)
+                continue
+            ga = got[g0 * wd:(g0 + n1 - n0) * wd].reshape(-1, wd)
+            wa = w[name][n0 * wd:n1 * wd].reshape(-1, wd)
+            if name in ("plus", "minus"):
+                ga, wa = ga[wet], wa[wet]
+            _compare(bad, name, ga, wa, acc)
+    return bad, acc[0], acc[1]
+
+
+def pristine(m, name, ntr):
+    """The pristine input `name` of all ntr tracers (tracer-slowest, as the batched handles hold
+    them), regenerated from the synthetic generator."""
+    if ntr == 1:
+        return synth.make_field(m, name, seed=43)
+    return np.concatenate([synth.make_field(m, name, seed=43 + k) for k in range(ntr)])
+
+
+def run_check_pass(args, e, step, m, ntr):
+    """One pass on pristine inputs (the outputs the timed steps overwrote are uploaded again)."""
+    for name in ("adf_v", "adf_h", "del_v", "del_h"):
+        e.upload(name, pristine(m, name, ntr))
+    step()
+    abi.device_sync()
+
+
+def verify_parallel(args, ctx, e, step, m, world, rank):
+    """The reference harness's verify-before-report (kernels/fct_ale_b2.py:97-100, ``answer=``) for the
+    structured meshes: one pass on pristine inputs, the outputs downloaded into memory-mapped files,
+    then ctx.pool's workers check row strips of this rank's domain (_check_strip); counts are summed
+    over the strips and over the ranks."""
+    ntr = args.tracers
+    nx, ny, nl = global_dims(args, world)
+    R0, R1 = partition.strip_rows(ny, world, rank) if world > 1 else (0, ny)
+    run_check_pass(args, e, step, m, ntr)
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    files, paths = {}, []
+    t0 = time.perf_counter()
+    try:
+        for name, _ in OUTPUTS:
+            n = e.size(name)
+            import tempfile
+            fd, path = tempfile.mkstemp(prefix=f"f2a_check_{os.getpid()}_{name}_", dir=shm)
+            os.close(fd)
+            paths.append(path)
+            buf = np.memmap(path, dtype=np.float64, mode="w+", shape=(max(n, 1),))
+            e.download(name, out=buf)
+            buf.flush()
+            del buf
+            files[name] = (path, (ntr, n // ntr))
+        # strips of about 80k nodes (a few seconds of oracle work each), at least one per worker
+        rows = R1 - R0
+        nstrip = max(min(rows, ctx.nworkers), min(rows, -(-(rows * nx) // 80000)))
+        cuts = [R0 + (rows * s) // nstrip for s in range(nstrip + 1)]
+        jobs = [(nx, ny, nl, not args.parity_levels, args.vlimit, (R0, R1), (cuts[s], cuts[s + 1]), ntr, files)
+                for s in range(nstrip) if cuts[s + 1] > cuts[s]]
+        res = ctx.pool.map(_check_strip, jobs, chunksize=1)
+    finally:
+        for p in paths:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+    t_oracle = time.perf_counter() - t0
+    bad, max_abs, cells = {}, 0.0, 0
+    for b_, mx, c in res:
+        for k, v in b_.items():
+            bad[k] = bad.get(k, 0) + v
+        max_abs, cells = max(max_abs, mx), cells + c
+    bad, max_abs, cells = reduce_check(ctx, bad, max_abs, cells)
+    return {"exact": not bad, "max_abs": max_abs, "mismatched_cells": bad, "cells_compared": cells,
+            "tracers": ntr, "ranks": world, "oracle_s": round(t_oracle, 1),
+            "against": f"oracle/fct_ale_oracle.c on {len(jobs)} row strips per rank, each widened by one ring "
+                       f"(exact without an exchange), {ctx.nworkers} worker processes per rank (per tracer)"}
+
+
+def reduce_check(ctx, bad, max_abs, cells):
+    if ctx.dist is None:
+        return bad, max_abs, cells
+    import torch
+    dist = ctx.dist
+    names = [k for k, _ in OUTPUTS]
+    v = torch.tensor([bad.get(k, 0) for k in names] + [cells], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    mx = torch.tensor([max_abs], dtype=torch.float64)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    return {k: int(n) for k, n in zip(names, v.tolist()[:-1]) if n}, float(mx.item()), int(v[-1].item())
+
+
+def verify(args, ctx, e, step, m, fields, world, lists, want=None):
+    """The serial verify-before-report (unstructured / permuted meshes, iter_yn, or the headline at
+    N = 1 where cpu_baseline's oracle pass is reused): one pass on the pristine inputs, then every
+    rank compares its owned cells (and local edges) with the oracle run on its own local mesh -- in
+    parallel on all ranks, the plus/minus halo exchanged over gloo for the oracle.  ``want``: the
+    oracle's outputs already computed for cpu_baseline (1 tracer, N = 1)."""
     for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h", "adf_v2", "adf_h2"):
         if name in e.host:
             e.upload(name)  # the host arrays were never touched in resident mode (adf_*2: zeros)
     step()
     abi.device_sync()
     ntr = len(fields)
-    got = {}
-    for name, width in (("plus", m.L), ("minus", m.L), ("del_v", m.L), ("del_h", m.L), ("adf_v", m.nl),
-                        ("adf_h", m.L)):
-        got[name] = e.download(name).reshape(ntr, -1)
+    got = {name: e.download(name).reshape(ntr, -1) for name, _ in OUTPUTS}
     t0 = time.perf_counter()
     if want is None:
-        want = oracle_local(m, fields, args, dist if world > 1 else None, lists)
+        want = oracle_local(m, fields, args, ctx.dist if world > 1 else None, lists)
     bad, max_abs, cells = compare_local(m, got, want)
     t_oracle = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        names = ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")
-        v = torch.tensor([bad.get(k, 0) for k in names] + [cells], dtype=torch.float64)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        mx = torch.tensor([max_abs], dtype=torch.float64)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        bad = {k: int(n) for k, n in zip(names, v.tolist()[:-1]) if n}
-        cells, max_abs = int(v[-1].item()), float(mx.item())
+    bad, max_abs, cells = reduce_check(ctx, bad, max_abs, cells)
     return {"exact": not bad, "max_abs": max_abs, "mismatched_cells": bad, "cells_compared": cells,
             "tracers": ntr, "ranks": world, "oracle_s": round(t_oracle, 1),
             "against": ("oracle/fct_ale_oracle.c pass on each rank's local mesh, plus/minus halo exchanged "
@@ -308,102 +503,35 @@ def verify(args, e, step, m, fields, world, dist, lists, want=None):
                         "oracle/fct_ale_oracle.c full pass on the same mesh (per tracer)")}
 
 
-def main():
-    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default=None, choices=list(synth.CONFIGS),
-                    help="default: 1.2M x 80 per GPU (weak), 9.6M x 80 in total (strong)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: the config per GPU; strong: the config split over the GPUs (SURVEY.md 8(e))")
-    ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
-    ap.add_argument("--mesh", default="structured", choices=["structured", "delaunay", "delaunay-hilbert"],
-                    help="delaunay: Delaunay triangulation of as many random points as the config has nodes "
-                         "(degrees 3..13, scattered numbering; 1 GPU); delaunay-hilbert: the same points "
-                         "numbered along a Hilbert curve (the locality of a renumbered FESOM2 mesh)")
-    ap.add_argument("--permuted", action="store_true",
-                    help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
-    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference", "reference-plain"],
-                    help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
-                         "stepwise: one kernel per reference step; reference: the reference's entry sequence "
-                         "pre_comm -> inter_comm -> post_comm -> c in its fast mode (fesom2_set_path_(2): b3v "
-                         "and the block-internal edges inside pre_comm); reference-plain: the same sequence without "
-                         "the fast mode (what a host that never calls fesom2_set_path_ gets)")
-    ap.add_argument("--tracers", type=int, default=1,
-                    help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture one step into a hipGraph after the warmup and time K replays (no host-side "
-                         "work per step; per-kernel timing and roofline are then not available)")
-    ap.add_argument("--transfers", action="store_true",
-                    help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
-                         "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
-                         "sequence; a PCIe-inclusive rate for DESIGN.md, not the benchmark value (1 GPU, 1 tracer)")
-    ap.add_argument("--vlimit", type=int, default=1, choices=[1, 2, 3],
-                    help="vertical limiter of a3 (docs/refactoring.md:113-148; reference.cpp has 1 only)")
-    ap.add_argument("--fct-iter", type=int, default=1,
-                    help="FESOM2's iterative FCT (iter_yn, SURVEY.md 8(f) 1): a step is K-1 rounds of "
-                         "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final pass (--path "
-                         "split: the direction-split entries, fused: pre_comm -> post_comm_c); 1 GPU")
-    ap.add_argument("--check", action="store_true", default=True,
-                    help="(default) after timing, rerun one pass on pristine inputs and compare every owned cell and "
-                         "local edge with the oracle on each rank's local mesh; the line carries \"check\" and the "
-                         "exit status is 1 on any mismatch")
-    ap.add_argument("--kernel-timing", default="dominant", choices=["all", "dominant", "none"],
-                    help="HIP events in the timed region around the dominant kernel only (default: the split "
-                         "pass's p1v; every other path times every launch), around every launch (all), or none "
-                         "(no roofline).  Each timed launch adds two events to the stream: at 127k x 47 timing "
-                         "every launch costs 5 %% of the pass.  With 'dominant' the other kernels are timed on "
-                         "a few extra steps after the timed region")
-    ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity check")
-    ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
-                    help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "
-                         "over gloo (validation only: lets N ranks share one GPU, which RCCL refuses)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
-    args = ap.parse_args()
-    if args.config is None:
-        args.config = "1.2M x 80" if args.scaling == "weak" else "9.6M x 80"
+# ----------------------------------------------------------------------------- one leg
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-
-    # all-cores CPU baseline first: its worker processes are spawned before this process touches
-    # the GPU
-    cpu_all = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_all = cpu_all_cores(args)
-        log(f"cpu all cores: {cpu_all}")
-
-    ceiling = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ceiling = stream_ceiling(args)  # own process, before this one touches the GPU
-        log(f"stream ceiling: {ceiling}")
-
-    abi.dll()  # engine first: one HIP runtime for the process
-    abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
+class Ctx:
+    """Per-process run state: rank, world, gloo group, worker pool, watchdog."""
+    rank = 0
+    world = 1
     dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        # gloo reports its connections on stdout; the driver reads rank 0's one JSON line there, so
-        # fd 1 goes to stderr while the group connects (for good on ranks other than 0)
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        dist.init_process_group("gloo")
-        dist.barrier()
-        sys.stdout.flush()
-        if rank == 0:
-            os.dup2(saved, 1)
-        os.close(saved)
+    pool = None
+    nworkers = 0
+    watchdog = None
 
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def allgather(self, values):
+        """[per rank: list of floats] over the gloo group."""
+        if self.dist is None:
+            return [list(values)]
+        import torch
+        t = torch.tensor(values, dtype=torch.float64)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
+
+
+def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
+    """Build, warm up, time K steps, break the kernels down, check.  Returns the leg's record."""
+    rank, world, dist = ctx.rank, ctx.world, ctx.dist
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
     if args.tracers > 1 and args.path in ("stepwise", "reference", "reference-plain"):
@@ -431,25 +559,37 @@ def main():
     abi.set_path({"stepwise": "stepwise", "reference": "reference"}.get(args.path, "fused"))
     dm = engine.DeviceMesh(m)
     dm.prepare()
-    mi = dm.info()
+    mi = dm.info(batched=args.tracers > 1)
     mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
     if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or args.transfers):
         raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
     e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
         engine.FctAleBatch(dm, fields, vlimit=args.vlimit)
+    parallel_check = (args.check and ctx.pool is not None and args.mesh == "structured" and not args.permuted
+                      and args.fct_iter == 1 and not args.transfers)
+    cpu_leg = headline and rank == 0 and world == 1 and not args.no_cpu_baseline
+    if parallel_check and not cpu_leg:
+        # the check regenerates its pristine inputs: no second host copy of the fields
+        e.drop_host()
+        del fields, f
+        fields = f = None
+        gc.collect()
     if args.path == "reference" and not args.transfers:
         e.bind_c_vertical()  # the fast mode's c-vertical inside pre_comm (fesom2_bind_c_vertical_)
     stream = e.stream
 
     halo = None
     if world > 1 and args.exchange == "rccl":
+        import torch
         uid = engine.Halo.unique_id() if rank == 0 else (C.c_char * 128)()
         t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
         dist.broadcast(t, src=0)
         C.memmove(uid, bytes(t.numpy().tobytes()), 128)
+        ctx.watchdog.arm(f"{args.leg}: RCCL communicator setup (ncclCommInitRank)", args.comm_timeout)
         halo = engine.Halo(uid, rank, world, lists, m.nl)
         ci = halo.info()
-        log(f"rank {rank}: owned {m.N} halo {m.H} neighbours {lists.neighbors} "
+        ctx.watchdog.disarm()
+        log(f"rank {rank}: {args.leg}: owned {m.N} halo {m.H} neighbours {lists.neighbors} "
             f"send {[lists.send[q].size for q in lists.neighbors]} recv {[lists.recv[q].size for q in lists.neighbors]} "
             f"rccl {ci}")
         if ci["nranks"] != world or ci["rank"] != rank:
@@ -467,7 +607,6 @@ def main():
         """FESOM2 with the reference's transfer semantics: the producer uploads ttf/adf_v/adf_h
         (src/fesom2-accelerate.cu:269-270), each phase moves its own fields, the host waits after
         phase 1 (where exchange_nod would run) and at the end."""
-        import ctypes as C
         for k in ("ttf", "adf_v", "adf_h"):
             abi.dll().transfer_var_async_(e.h[k].ref, abi.arr(e.host[k]), e.stream.ref, C.byref(C.c_bool(True)))
         if e.pre_comm() != 6:
@@ -514,10 +653,13 @@ def main():
         if s2 != 9:
             raise RuntimeError(f"phase 2 alg_state {s2}: {abi.last_error()}")
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
+    # the first step carries the first exchange: bounded on every rank (a stalled RCCL send/recv)
+    if world > 1:
+        ctx.watchdog.arm(f"{args.leg}: first step (first halo exchange)", args.comm_timeout)
+        step()
+        abi.device_sync()
+        ctx.barrier()
+        ctx.watchdog.disarm()
     for _ in range(args.warmup):
         step()
     abi.device_sync()
@@ -542,7 +684,7 @@ def main():
     timed_only = args.kernel_timing == "dominant" and args.path == "split" and args.fct_iter == 1 and not args.graph
     abi.kernel_timing_only("fct_ale_p1v" if timed_only else None)
     abi.kernel_timing_reset()
-    barrier()
+    ctx.barrier()
     abi.device_sync()
     ev0, ev1 = abi.Event(), abi.Event()
     ev0.record(stream)
@@ -552,15 +694,18 @@ def main():
     ev1.record(stream)
     abi.device_sync()
     t1 = time.perf_counter()
-    barrier()
+    ctx.barrier()
     abi.kernel_timing(False)
-    wall = t1 - t0
+    wall_rank = t1 - t0
     gpu_ms = ev0.elapsed_ms(ev1)
+    ev0.free()
+    ev1.free()
     stats = abi.kernel_stats()
     breakdown = {}
-    if timed_only:
-        # the per-kernel breakdown, outside the timed region: a few more steps with every launch timed
-        # (every rank runs them: the N > 1 step contains the exchange)
+    if timed_only or world > 1:
+        # the per-kernel breakdown (and at N > 1 the halo exchange's own time and its exposed wait),
+        # outside the timed region: a few more steps with every launch timed (every rank runs them:
+        # the N > 1 step contains the exchange)
         abi.kernel_timing_only(None)
         abi.kernel_timing(True)
         abi.kernel_timing_reset()
@@ -569,33 +714,30 @@ def main():
         abi.device_sync()
         abi.kernel_timing(False)
         breakdown = abi.kernel_stats()
+        ctx.barrier()
 
-    if dist is not None:
-        import torch
-        tt = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
-        cells = torch.tensor([mesh_stats(m)["cn"]], dtype=torch.float64)
-        dist.all_reduce(cells, op=dist.ReduceOp.SUM)
-        total_cells = float(cells.item())
-    else:
-        total_cells = float(mesh_stats(m)["cn"])
-
+    s = mesh_stats(m)
+    s.update(mesh_info)
+    # per-rank spread (max over ranks is the step time) and the exchange's own timing
+    avg = lambda st, k: st[k][1] / st[k][0] if k in st and st[k][0] else 0.0
+    per_rank = ctx.allgather([1e3 * wall_rank / args.steps, avg(stats, "fct_ale_p1v"),
+                              avg(breakdown, "halo_exchange"), avg(breakdown, "halo_wait"), float(s["cn"])])
+    wall = max(r[0] for r in per_rank) * args.steps / 1e3
+    total_cells = sum(r[4] for r in per_rank)
     ms_step = 1e3 * wall / args.steps
     value = args.tracers * total_cells / (wall / args.steps)  # tracer cell-updates
 
     # ---- roofline of the dominant kernel (rank-local, all ranks do the same work)
-    s = mesh_stats(m)
-    s.update(mesh_info)
     kb = kernel_bytes(s, args.tracers, split=args.path in ("split", "reference"))
+    kbm = kernel_bytes_min(s, args.tracers)
     per_kernel = {}
     for name, (cnt, tot) in list(stats.items()) + [kv for kv in breakdown.items() if kv[0] not in stats]:
-        avg = tot / max(cnt, 1)
-        entry = {"launches": cnt, "avg_ms": round(avg, 4),
+        a_ms = tot / max(cnt, 1)
+        entry = {"launches": cnt, "avg_ms": round(a_ms, 4),
                  "timed": "timed region" if name in stats else "extra steps after the timed region"}
         if name in kb:
             entry["alg_bytes"] = kb[name]
-            entry["GBps"] = round(kb[name] / (avg * 1e-3) / 1e9, 1)
+            entry["GBps"] = round(kb[name] / (a_ms * 1e-3) / 1e9, 1)
         per_kernel[name] = entry
     dom = max(stats, key=lambda k: stats[k][1]) if stats else None
     traffic = None
@@ -609,7 +751,7 @@ def main():
             continue
         if tr.get("workload") == args.config and tr.get("tracers", 1) == args.tracers and \
                 args.mesh == "structured" and not args.parity_levels and args.vlimit == 1 and \
-                args.fct_iter == 1 and dom in tr.get("bytes_per_launch", {}):
+                args.fct_iter == 1 and args.scaling == "weak" and dom in tr.get("bytes_per_launch", {}):
             traffic = tr["bytes_per_launch"][dom]
             break
     roof = None
@@ -618,7 +760,16 @@ def main():
         achieved = kb[dom] / avg_s / 1e9
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s", "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic,
-                "alg_bytes_per_launch": kb[dom], "avg_launch_ms": round(avg_s * 1e3, 4)}
+                "alg_bytes_per_launch": kb[dom], "avg_launch_ms": round(avg_s * 1e3, 4),
+                "byte_model": "alg_bytes_per_launch: the kernel's own arrays, halo columns, internal-edge "
+                              "flux writes and index arrays once each (DESIGN.md 3)"}
+        if dom in kbm:
+            roof["alg_bytes_min"] = kbm[dom]
+            roof["frac_min"] = round(kbm[dom] / avg_s / HBM_PEAK, 4)
+            roof["byte_model_min"] = "alg_bytes_min: SURVEY.md 8(d)'s strict minimum for the same work " \
+                                     "(p1v: 32 Cn + ntracers (64 Cn + 8 Ce); p1: 8 Cn + ntracers (40 Cn + 8 Ce))"
+        if traffic:
+            roof["traffic_over_alg"] = round(traffic / kb[dom], 3)
         if ceiling:  # context: what this GPU streams (copy) and streams in p1v's pattern, same run
             roof["stream_ceiling"] = dict(ceiling, frac_of_copy=round(achieved / ceiling["copy_GBps"], 4),
                                           tool="tools/stream_probe.hip")
@@ -626,10 +777,10 @@ def main():
                 roof["stream_ceiling"]["frac_of_p1v_pattern"] = round(achieved / ceiling["p1v_pattern_GBps"], 4)
     pass_gbs = kb["survey_pass"] / (ms_step * 1e-3) / 1e9
 
-    # ---- CPU baseline (rank 0, N = 1 only)
+    # ---- CPU baseline (rank 0, N = 1, headline only)
     cpu = None
     oracle_want = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if cpu_leg:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
         best, reps, last = O.time_full_pass(m, f, budget_s=args.cpu_budget, keep=True)
@@ -649,61 +800,266 @@ def main():
 
     check = None
     if args.check and not args.transfers:  # --transfers: outputs land in the input host arrays
-        check = verify(args, e, step, m, fields, world, dist, lists, oracle_want)  # a replay when --graph
-        log(f"check: {check}")
+        if parallel_check and oracle_want is None:
+            check = verify_parallel(args, ctx, e, step, m, world, rank)  # a replay when --graph
+        else:
+            check = verify(args, ctx, e, step, m, fields, world, lists, oracle_want)
+        log(f"check ({args.leg}): {check}")
     if graph is not None:
         graph.free()
 
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "cell-updates/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
-            "config": {"workload": f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}"
-                                   + {"structured": "", "delaunay": " Delaunay mesh",
-                                      "delaunay-hilbert": " Delaunay mesh, Hilbert numbering"}[args.mesh]
-                                   + (" per GPU" if args.scaling == "weak" else f" split over {world} GPU(s)")
-                                   + f", {args.tracers} tracer{'s' if args.tracers > 1 else ''}"
-                                   + (" (batched)" if args.tracers > 1 else ""),
-                       "tracers": args.tracers, "vlimit": args.vlimit, "fct_iterations": args.fct_iter,
-                       "nodes_per_gpu": m.N, "levels": m.L,
-                       "global_nodes": global_dims(args, world)[0] * global_dims(args, world)[1],
-                       "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
-                       "parallelism": (f"node partition y-strips x{world}, "
-                                       + ("RCCL halo overlapped with interior phase 2" if args.exchange == "rccl"
-                                          else "host/gloo halo (validation, not a benchmark)"))
-                       if world > 1 else "1 GPU",
-                       "path": args.path},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "pass_roofline": {"alg_bytes": kb["survey_pass"], "GBps": round(pass_gbs, 1),
-                              "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
-                              "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
-            "kernels": per_kernel,
-            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
-            "graph": bool(args.graph),
-            "transfers": "reference transfer semantics, PCIe inside the timed step" if args.transfers else
-                         "device resident (inputs in HBM before the timed region)",
-            "setup_s": round(setup_s, 1),
-        }
-        if check is not None:
-            out["check"] = check
-        if halo is not None:
-            ci = halo.info()
-            out["rccl_nranks"] = ci["nranks"]  # ncclCommCount of the communicator the exchange ran on
-            out["rccl"] = ci
-        print(json.dumps(out), flush=True)
-
+    rec = {"value": round(value, 1), "ms_per_step": round(ms_step, 4), "roofline": roof,
+           "pass_roofline": {"alg_bytes": kb["survey_pass"], "GBps": round(pass_gbs, 1),
+                             "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
+                             "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
+           "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+           "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s}
+    if world > 1:
+        ms = [r[0] for r in per_rank]
+        rec["ranks"] = {
+            "ms_per_step": [round(x, 4) for x in ms], "ms_per_step_min": round(min(ms), 4),
+            "ms_per_step_max": round(max(ms), 4), "spread": round(max(ms) / min(ms) - 1, 4) if min(ms) else None,
+            "p1v_avg_ms": [round(r[1], 4) for r in per_rank],
+            "halo_exchange_ms": [round(r[2], 4) for r in per_rank],
+            "halo_wait_ms": [round(r[3], 4) for r in per_rank],
+            "halo_hidden_frac": [round(max(0.0, min(1.0, 1 - r[3] / r[2])), 4) if r[2] else None for r in per_rank],
+            "timing": "ms_per_step: timed region per rank (value uses the max); halo_exchange_ms: pack + grouped "
+                      "RCCL send/recv + unpack on the halo stream, halo_wait_ms: the compute stream's wait for it "
+                      "after the interior work (the exposed part), both from HIP events on extra steps after the "
+                      "timed region"}
+    if halo is not None:
+        ci = halo.info()
+        rec["rccl_nranks"] = ci["nranks"]  # ncclCommCount of the communicator the exchange ran on
+        rec["rccl"] = ci
     e.free()
     dm.free()
     for hp in pinned:
         abi.dll().fesom2_free_pinned_(C.byref(hp))
     if halo is not None:
         halo.free()
-    if dist is not None:
-        dist.destroy_process_group()
-    if check is not None and not check["exact"]:
+    return rec
+
+
+def workload_name(args, world, m):
+    return (f"{args.config} {'parity levels' if args.parity_levels else 'full-depth'}"
+            + {"structured": "", "delaunay": " Delaunay mesh", "delaunay-hilbert": " Delaunay mesh, Hilbert numbering"}[args.mesh]
+            + (" per GPU" if args.scaling == "weak" else f" split over {world} GPU(s)")
+            + f", {args.tracers} tracer{'s' if args.tracers > 1 else ''}" + (" (batched)" if args.tracers > 1 else ""))
+
+
+def extra_legs(args, world):
+    """The further BASELINE configs measured in the same run (--extras auto)."""
+    strong = ("config4_strong_" + args.strong_config.replace(" ", "").replace(".", "p"),
+              dict(config=args.strong_config, tracers=1, scaling="strong"))
+    if world == 1:
+        return [("config1_127kx47", dict(config="127k x 47", tracers=1, scaling="weak")),
+                ("config1_127kx47_6tracers", dict(config="127k x 47", tracers=6, scaling="weak")),
+                ("config3_1p2Mx80_6tracers", dict(config="1.2M x 80", tracers=6, scaling="weak")),
+                strong]
+    return [strong]
+
+
+def compact(rec, args, world):
+    """An extra leg's sub-record."""
+    m, s = rec["m"], rec["s"]
+    out = {"workload": workload_name(args, world, m), "scaling": args.scaling, "value": rec["value"],
+           "unit": "cell-updates/s" if args.tracers == 1 else "tracer-cell-updates/s",
+           "ms_per_step": rec["ms_per_step"], "steps": args.steps, "warmup": args.warmup,
+           "nodes_per_gpu": m.N, "levels": m.L, "cells_per_gpu": s["cn"], "tracers": args.tracers,
+           "roofline": rec["roofline"], "pass_roofline": rec["pass_roofline"],
+           "kernels_ms": {k: v["avg_ms"] for k, v in rec["kernels"].items()}, "check": rec["check"],
+           "setup_s": rec["setup_s"]}
+    for k in ("ranks", "rccl_nranks"):
+        if k in rec:
+            out[k] = rec[k]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default=None, choices=list(synth.CONFIGS),
+                    help="default: 1.2M x 80 per GPU (weak), 9.6M x 80 in total (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: the config per GPU; strong: the config split over the GPUs (SURVEY.md 8(e))")
+    ap.add_argument("--parity-levels", action="store_true", help="random element levels instead of full depth")
+    ap.add_argument("--mesh", default="structured", choices=["structured", "delaunay", "delaunay-hilbert"],
+                    help="delaunay: Delaunay triangulation of as many random points as the config has nodes "
+                         "(degrees 3..13, scattered numbering; 1 GPU); delaunay-hilbert: the same points "
+                         "numbered along a Hilbert curve (the locality of a renumbered FESOM2 mesh)")
+    ap.add_argument("--permuted", action="store_true",
+                    help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
+    ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference", "reference-plain"],
+                    help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
+                         "stepwise: one kernel per reference step; reference: the reference's entry sequence "
+                         "pre_comm -> inter_comm -> post_comm -> c in its fast mode (fesom2_set_path_(2): b3v "
+                         "and the block-internal edges inside pre_comm); reference-plain: the same sequence without "
+                         "the fast mode (what a host that never calls fesom2_set_path_ gets)")
+    ap.add_argument("--tracers", type=int, default=1,
+                    help="tracers per pass; > 1 uses the batched entry points (BASELINE config 3: 6)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one step into a hipGraph after the warmup and time K replays (no host-side "
+                         "work per step; per-kernel timing and roofline are then not available)")
+    ap.add_argument("--transfers", action="store_true",
+                    help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
+                         "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
+                         "sequence; a PCIe-inclusive rate for DESIGN.md, not the benchmark value (1 GPU, 1 tracer)")
+    ap.add_argument("--vlimit", type=int, default=1, choices=[1, 2, 3],
+                    help="vertical limiter of a3 (docs/refactoring.md:113-148; reference.cpp has 1 only)")
+    ap.add_argument("--fct-iter", type=int, default=1,
+                    help="FESOM2's iterative FCT (iter_yn, SURVEY.md 8(f) 1): a step is K-1 rounds of "
+                         "pre_comm -> post_comm_iter (LO update, remainder fluxes) then the final pass (--path "
+                         "split: the direction-split entries, fused: pre_comm -> post_comm_c); 1 GPU")
+    ap.add_argument("--check", action="store_true", default=True,
+                    help="(default) after timing, rerun one pass on pristine inputs and compare every owned cell and "
+                         "local edge with the oracle; the line carries \"check\" and the exit status is 1 on any "
+                         "mismatch")
+    ap.add_argument("--kernel-timing", default="dominant", choices=["all", "dominant", "none"],
+                    help="HIP events in the timed region around the dominant kernel only (default: the split "
+                         "pass's p1v; every other path times every launch), around every launch (all), or none "
+                         "(no roofline).  Each timed launch adds two events to the stream: at 127k x 47 timing "
+                         "every launch costs 5 %% of the pass.  With 'dominant' the other kernels are timed on "
+                         "a few extra steps after the timed region")
+    ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity check")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
+                    help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "
+                         "over gloo (validation only: lets N ranks share one GPU, which RCCL refuses)")
+    ap.add_argument("--extras", default="auto", choices=["auto", "on", "none"],
+                    help="auto (default): with the default workload also measure the other BASELINE configs in "
+                         "this run (N = 1: 127k x 47 with 1 and 6 tracers, 1.2M x 80 with 6 tracers, 9.6M x 80 on "
+                         "one GPU; N > 1: 9.6M x 80 split over the N GPUs) as 'extra' sub-records; on: whatever the "
+                         "headline workload (e.g. with --exchange host, to rehearse N > 1 on one GPU)")
+    ap.add_argument("--strong-config", default="9.6M x 80", choices=list(synth.CONFIGS),
+                    help="the strong-scaling leg's global mesh (BASELINE configs[4]: 9.6M x 80)")
+    ap.add_argument("--comm-timeout", type=float, default=180.0,
+                    help="watchdog bound (s) of RCCL communicator setup and of the first exchange step")
+    ap.add_argument("--leg-timeout", type=float, default=900.0, help="watchdog bound (s) of each extra leg")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
+    args = ap.parse_args()
+    default_workload = args.config is None and args.scaling == "weak" and args.tracers == 1 and \
+        args.mesh == "structured" and not (args.permuted or args.parity_levels or args.graph or args.transfers) and \
+        args.vlimit == 1 and args.fct_iter == 1 and args.path == "split" and args.exchange == "rccl"
+    if args.config is None:
+        args.config = "1.2M x 80" if args.scaling == "weak" else "9.6M x 80"
+    args.leg = "headline"
+
+    ctx = Ctx()
+    ctx.world = world = int(os.environ.get("WORLD_SIZE", "1"))
+    ctx.rank = rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    ctx.watchdog = Watchdog(rank)
+
+    # worker pool and the all-cores CPU baseline first: their processes are spawned before this
+    # process touches the GPU
+    if args.check or (rank == 0 and world == 1 and not args.no_cpu_baseline):
+        ctx.pool, ctx.nworkers = make_pool(world)
+    cpu_all = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_all = cpu_all_cores(args, ctx.pool, ctx.nworkers)
+        log(f"cpu all cores: {cpu_all}")
+
+    ceiling = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ceiling = stream_ceiling(args)  # own process, before this one touches the GPU
+        log(f"stream ceiling: {ceiling}")
+
+    abi.dll()  # engine first: one HIP runtime for the process
+    abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
+    if world > 1:
+        import torch.distributed as dist
+        # gloo reports its connections on stdout; the driver reads rank 0's one JSON line there, so
+        # fd 1 goes to stderr while the group connects (for good on ranks other than 0)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        ctx.watchdog.arm("gloo process group setup", args.comm_timeout)
+        dist.init_process_group("gloo")
+        dist.barrier()
+        ctx.watchdog.disarm()
+        sys.stdout.flush()
+        if rank == 0:
+            os.dup2(saved, 1)
+        os.close(saved)
+        ctx.dist = dist
+
+    head = run_leg(args, ctx, headline=True, cpu_all=cpu_all, ceiling=ceiling)
+    m, s = head["m"], head["s"]
+    out = {
+        "metric": METRIC, "value": head["value"], "unit": "cell-updates/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (deterministic splitmix64 fields, periodic structured triangulation; no dataset)",
+        "config": {"workload": workload_name(args, world, m),
+                   "tracers": args.tracers, "vlimit": args.vlimit, "fct_iterations": args.fct_iter,
+                   "nodes_per_gpu": m.N, "levels": m.L,
+                   "global_nodes": global_dims(args, world)[0] * global_dims(args, world)[1],
+                   "cells_per_gpu": s["cn"], "edge_cells_per_gpu": s["ce"],
+                   "parallelism": (f"node partition y-strips x{world}, "
+                                   + ("RCCL halo overlapped with interior phase 2" if args.exchange == "rccl"
+                                      else "host/gloo halo (validation, not a benchmark)"))
+                   if world > 1 else "1 GPU",
+                   "path": args.path},
+        "roofline": head["roofline"],
+        "cpu_baseline": head["cpu"],
+        "pass_roofline": head["pass_roofline"],
+        "kernels": head["kernels"],
+        "gpu_event_ms_per_step": head["gpu_event_ms_per_step"],
+        "graph": bool(args.graph),
+        "transfers": "reference transfer semantics, PCIe inside the timed step" if args.transfers else
+                     "device resident (inputs in HBM before the timed region)",
+        "setup_s": head["setup_s"],
+    }
+    if head["check"] is not None:
+        out["check"] = head["check"]
+    for k in ("ranks", "rccl_nranks", "rccl"):
+        if k in head:
+            out[k] = head[k]
+    del head, m, s
+    gc.collect()
+    exact = out.get("check") is None or out["check"]["exact"]
+
+    # ---- further BASELINE configs in the same run
+    if (default_workload and args.extras == "auto") or args.extras == "on":
+        out["extra"] = {}
+
+        def partial(stage):  # watchdog on rank 0: the headline is measured, print what there is
+            if rank == 0:
+                out["extra"]["error"] = f"watchdog: '{stage}' not done within its bound"
+                print(json.dumps(out), flush=True)
+        ctx.watchdog.on_fire = partial
+        for name, over in extra_legs(args, world):
+            la = copy.copy(args)
+            for k, v in over.items():
+                setattr(la, k, v)
+            la.leg = name
+            la.traffic = os.path.join(ROOT, "profiles", "none.json")  # the per-config traffic files below
+            ctx.watchdog.arm(f"extra leg {name}", args.leg_timeout)
+            t0 = time.perf_counter()
+            rec = run_leg(la, ctx)
+            ctx.watchdog.disarm()
+            out["extra"][name] = compact(rec, la, world)
+            out["extra"][name]["leg_s"] = round(time.perf_counter() - t0, 1)
+            exact = exact and (rec["check"] is None or rec["check"]["exact"])
+            del rec
+            gc.collect()
+            log(f"extra {name}: {out['extra'][name]['ms_per_step']} ms/step")
+        ctx.watchdog.on_fire = None
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
+    if ctx.pool is not None:
+        ctx.pool.terminate()
+    if not exact:
         sys.exit(1)  # a fast wrong answer is not a result
 
 

@@ -84,6 +84,10 @@ Buffer *need(void **h, size_t bytes, const char *name)
         report("%s holds %zu bytes, the call needs %zu", name, b->size, bytes);
         return nullptr;
     }
+    if (b && b->pad < kAllocPad) {
+        report("%s has no %zu bytes of slack behind its end (not allocated by this library)", name, kAllocPad);
+        return nullptr;
+    }
     return b;
 }
 
@@ -107,6 +111,7 @@ Buffer *allocate(void *host, size_t bytes, bool create_event)
         delete m;
         return nullptr;
     }
+    m->pad = kAllocPad;
     if (create_event) {
         if (!ok(hipEventCreateWithFlags(&m->event, hipEventDisableTiming), "hipEventCreate")) {
             (void)hipFree(m->device_pointer);
@@ -366,9 +371,10 @@ bool marks_replayable(const CaptureLog &log)
     for (const CapturedMark &m : log.marks)
         if (m.read_first && object_live(m.b, m.serial) &&
             (m.b->int_plan != m.entry || m.b->int_serial != m.entry_serial)) {
-            report("fesom2_graph_launch_: the graph's first use of fct_adf_h expects it %s by "
-                   "fct_ale_pre_comm_v_acc_, but it is %s now (run the matching phase first, or capture both)",
-                   m.entry ? "marked" : "not marked", m.b->int_plan ? "marked" : "not marked");
+            report("fesom2_graph_launch_: the graph first reads a phase mark on buffer %p (fct_adf_h, fct_adf_v or "
+                   "del_ttf_advvert) and expects it %s by the phase-1 call that sets it, but it is %s now (run the "
+                   "matching phase first, or capture both)",
+                   (const void *)m.b, m.entry ? "marked" : "not marked", m.b->int_plan ? "marked" : "not marked");
             return false;
         }
     return true;

@@ -46,6 +46,10 @@ struct Buffer {
     void *host_pointer = nullptr;
     void *device_pointer = nullptr;
     size_t size = 0;  // bytes
+    // readable slack behind `size` (kAllocPad for every array allocate() makes): need() refuses a
+    // buffer without it, so an entry that ever wraps a foreign device pointer (an OpenACC/OpenMP
+    // array of the host) fails loudly instead of letting the odd-L pair loads read past its end
+    size_t pad = 0;
     hipEvent_t event = nullptr;
     bool has_event = false;
     uint64_t serial = 0;  // live-object serial (track_object): graph replays check it is unchanged

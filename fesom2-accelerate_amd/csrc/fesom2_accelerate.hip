@@ -246,6 +246,12 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
                 }
     };
 
+    // every path: fluxes a phase-1 call already limited in part (fast mode, pre_comm_v) are refused
+    if (has_internal(badfv, st) || has_internal(badfh, st)) {
+        report("fct_ale_pre_comm_acc_: fct_adf_v/fct_adf_h already hold a limited phase 2 part (upload "
+               "the raw fluxes first)");
+        return;
+    }
     if (!stepwise) {
         f2a::P1Args a{N, NL, *vlimit, nlev_nod, dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
                       dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
@@ -253,11 +259,6 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         if (kernel_path() == 2) {
             // fast mode: b3-vertical (and the block-internal edges' b3-horizontal) while the block's
             // plus/minus are in LDS; inter_comm / post_comm find the marks and do the rest
-            if (has_internal(badfv, st) || has_internal(badfh, st)) {
-                report("fct_ale_pre_comm_acc_: fct_adf_v/fct_adf_h already hold a limited phase 2 part (upload "
-                       "the raw fluxes first)");
-                return;
-            }
             Buffer *cvb[4] = {nullptr, nullptr, nullptr, nullptr};
             if (!bound_c_vertical(badfv, N, L, NL, cvb)) return;
             if (cvb[0]) {  // c-vertical too (fesom2_bind_c_vertical_)
@@ -364,6 +365,13 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
         if (!barea || !bh || !bhn || !bdv) return;
     }
     mh.nlev_nod = bnlnod;
+    // fluxes a fast-mode fct_ale_pre_comm_acc_ (or an unfinished pre_comm_v) already limited in part:
+    // limiting them again would be wrong -- the same guard as the fast mode's own
+    if (has_internal(badfv, st) || has_internal(badfh, st) || (bdv && has_internal(bdv, st))) {
+        report("%s: fct_adf_v/fct_adf_h/del_ttf_advvert already hold a limited phase 2 part (finish that "
+               "phase, or upload the raw fluxes first)", who);
+        return;
+    }
     const Plan *plan = get_plan(mh, N, NT, E, NL, true, ntr > 1);
     if (!plan) return;
     if (!g_resident && !h2d(blo, false, st, false)) return;
@@ -557,6 +565,19 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
         return;
     }
     if (has_internal(bdv, st)) {
+        // c-vertical was done by pre_comm on the bound fields: they must be this call's, on this mesh
+        const CvBinding *cv = badfv->cv;
+        if (!cv || cv->b[0] != bdv || cv->b[1] != bh || cv->b[2] != bhn || cv->b[3] != barea) {
+            report("fct_ale_c_acc_: del_ttf_advvert holds c-vertical of fields other than this call's "
+                   "hnode/hnode_new/area (fesom2_bind_c_vertical_ bound others)");
+            return;
+        }
+        const Plan *vp = peek_internal(bdv, st);
+        if (!vp || vp->dev.n_owned != N || vp->dev.nl != NL) {
+            report("fct_ale_c_acc_: del_ttf_advvert was updated on another mesh (myDim_nod2D = %d, nl = %d here)", N,
+                   NL);
+            return;
+        }
         // the fast mode's fct_ale_pre_comm_acc_ did c-vertical already: c-horizontal only
         f2a::P2Args a{NL, d.p2_rec, N, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dptr<real>(barea), nullptr,
                       dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import bench
-from fesom2_amd import synth
+from fesom2_amd import partition, synth
 
 
 @pytest.fixture(scope="module")
@@ -137,3 +137,88 @@ def test_per_rank_oracle_with_gloo_halo_equals_single_domain():
             for name, w in (("plus", L), ("minus", L), ("del_v", L), ("del_h", L), ("adf_v", g.nl)):
                 assert np.array_equal(o[name].reshape(-1, w)[:n], want[name].reshape(-1, w)[gid]), (rank, k, name)
             assert np.array_equal(o["adf_h"].reshape(-1, L), want["adf_h"].reshape(-1, L)[egid]), (rank, k)
+
+
+# ----------------------------------------------------------------------------- parallel strip check
+
+def _rank_outputs(g, m, ntr):
+    """What the GPU of rank-local mesh m would hold after a pass: the single-domain oracle's values
+    on its owned nodes / local edges (halo parts arbitrary), laid out as the handles (tracer-slowest)."""
+    import oracle as O
+    L, nl = g.L, g.nl
+    out = {k: [] for k, _ in bench.OUTPUTS}
+    NT = m.N + m.H
+    for f in synth.make_tracer_fields(g, ntr):
+        w = O.full_pass(g, f)
+        for name, width in bench.OUTPUTS:
+            wd = L if width == "L" else nl
+            if name == "adf_h":
+                a = w[name].reshape(-1, wd)[m.edge_gid]
+            else:
+                a = np.full((NT, wd), 7.0)
+                a[: m.N] = w[name].reshape(-1, wd)[m.node_gid[: m.N]]
+            out[name].append(a.reshape(-1))
+    return {k: np.stack(v) for k, v in out.items()}
+
+
+@pytest.mark.parametrize("world,ntr,full", [(1, 1, False), (2, 2, False), (3, 1, True)])
+def test_parallel_strip_check_is_exact_and_counts_each_cell_once(tmp_path, world, ntr, full):
+    """bench.py's parallel check: the oracle on row strips widened by one ring equals the
+    single-domain pass on the strip's rows and edges (no exchange), every local edge is compared by
+    exactly one strip, and a changed cell is reported once."""
+    nx, ny, nl = 24, 17, 9
+    g = synth.make_mesh(nx, ny, nl, full_depth=full)
+    for rank in range(world):
+        R0, R1 = partition.strip_rows(ny, world, rank)
+        m, _ = partition.strip_local_mesh(nx, ny, nl, R0, R1, full_depth=full)
+        got = _rank_outputs(g, m, ntr)
+        s = bench.mesh_stats(m)
+        wet = int(s["cn"])
+
+        def run(arrs):
+            files = {}
+            for name, a in arrs.items():
+                p = tmp_path / f"{rank}_{name}"
+                mm = np.memmap(p, dtype=np.float64, mode="w+", shape=a.shape)
+                mm[:] = a
+                mm.flush()
+                files[name] = (str(p), a.shape)
+            cuts = [R0, R0 + (R1 - R0) // 3, R0 + 2 * (R1 - R0) // 3, R1]
+            res = [bench._check_strip((nx, ny, nl, full, 1, (R0, R1), (cuts[k], cuts[k + 1]), ntr, files))
+                   for k in range(3) if cuts[k + 1] > cuts[k]]
+            bad, cells = {}, 0
+            for b_, _, c in res:
+                for k_, v in b_.items():
+                    bad[k_] = bad.get(k_, 0) + v
+                cells += c
+            return bad, cells
+
+        bad, cells = run(got)
+        assert not bad, (rank, bad)
+        assert cells == ntr * (2 * wet + 2 * m.N * m.L + m.N * nl + m.E * m.L), (rank, cells)
+        got["adf_h"][ntr - 1, 5 * m.L + 1] += 1.0
+        got["del_v"][0, 3] = np.nan
+        bad, _ = run(got)
+        assert bad == {"adf_h": 1, "del_v": 1}, bad
+
+
+def test_kernel_bytes_min_is_the_survey_minimum(stats):
+    """alg_bytes_min of p1v = phase 1 (48 Cn + 8 Ce) + the vertical half of phase 2 (48 Cn) at one
+    tracer, mesh fields once per batch."""
+    _, s = stats
+    one = bench.kernel_bytes_min(s, 1)
+    assert one["fct_ale_p1v"] == 96 * s["cn"] + 8 * s["ce"]
+    assert one["fct_ale_p1"] == 48 * s["cn"] + 8 * s["ce"]
+    six = bench.kernel_bytes_min(s, 6)
+    assert six["fct_ale_p1v"] == 32 * s["cn"] + 6 * (64 * s["cn"] + 8 * s["ce"])
+    # the kernel's own model counts halo columns, index arrays and internal-edge writes on top
+    assert bench.kernel_bytes(s, 1, split=True)["fct_ale_p1v"] > one["fct_ale_p1v"]
+
+
+def test_watchdog_exits_with_the_stage_on_stderr():
+    """A stalled stage ends the rank (status 3) and names the stage."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; w = bench.Watchdog(5); "
+            "w.arm('RCCL communicator setup', 1.0); time.sleep(30)") % bench.ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 3
+    assert "rank 5: watchdog: stage 'RCCL communicator setup' not done within 1 s" in out.stderr

@@ -694,6 +694,58 @@ def test_fast_mode_c_vertical_binding_checks():
         dm.free()
 
 
+def test_fast_mode_marks_refuse_a_split_pre_comm():
+    """after a fast-mode fct_ale_pre_comm_acc_ (b3v, the internal edges and with the
+    binding c-vertical done) the split entry fct_ale_pre_comm_v_acc_ and the batched/fused phase 1
+    refuse the marked fluxes instead of limiting them a second time; fresh uploads clear the marks."""
+    m, f = mesh("8k x 20", full_depth=True)
+    want = O.full_pass(m, f)
+    abi.set_path("reference")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        e.bind_c_vertical()
+        assert e.pre_comm() == 6, abi.last_error()
+        assert e.pre_comm_v() != 7 and "already hold a limited" in abi.last_error()
+        abi.set_path("fused")
+        assert e.pre_comm() != 6 and "already hold a limited" in abi.last_error()
+        for k in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(k)
+        assert e.split_pass() == 9, abi.last_error()
+        e.sync()
+        for k in ("del_v", "del_h", "adf_v", "adf_h"):
+            assert np.array_equal(e.download(k), want[k]), k
+    finally:
+        abi.set_path("fused")
+        e.bind_c_vertical(False)
+        e.free()
+        dm.free()
+
+
+def test_fast_mode_c_step_checks_every_bound_field():
+    """with c-vertical done in the fast-mode pre_comm, a c-step given other hnode /
+    hnode_new / area handles than the bound ones is refused (c-vertical and c-horizontal would use
+    different fields)."""
+    m, f = mesh("8k x 20")
+    abi.set_path("reference")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        e.bind_c_vertical()
+        assert e.pre_comm() == 6 and e.inter_comm() == 7 and e.post_comm() == 8, abi.last_error()
+        h = e.h
+        for k, other in (("hnode", "hnode_new"), ("hnode_new", "hnode"), ("area", "area_inv")):
+            e.h = dict(h, **{k: h[other]})
+            assert e.c_step() != 9 and "bound others" in abi.last_error(), k
+        e.h = h
+        assert e.c_step() == 9, abi.last_error()
+    finally:
+        abi.set_path("fused")
+        e.bind_c_vertical(False)
+        e.free()
+        dm.free()
+
+
 def test_kernel_timing_only_times_the_named_kernel():
     """fesom2_kernel_timing_only_ (bench.py --kernel-timing dominant): while a name is set only that
     kernel's launches get events; with None every launch of the split pass is timed again.  Results

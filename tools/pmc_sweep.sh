@@ -12,7 +12,7 @@ for cfg in "$@"; do
   d=gpurun_out/pmcs_$i
   rm -rf $d && mkdir -p $d
   eval "env $cfg timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum \
-      --output-format csv -d $d/rd -o rd -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 $BENCH_ARGS" \
+      --output-format csv -d $d/rd -o rd -- python3 bench.py --no-cpu-baseline --no-check --extras none --steps 3 --warmup 1 $BENCH_ARGS" \
       > $d/bench.json 2> $d/err.log
   python3 - "$cfg" $d >> $out <<'PY'
 import csv, collections, glob, json, sys

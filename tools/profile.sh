@@ -9,11 +9,11 @@ eval "args=(${BENCH_ARGS:-})"
 out=gpurun_out/prof_$tag
 rm -rf "$out" && mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d "$out/stats" -o run -- \
-    python3 bench.py --no-cpu-baseline --no-check "${args[@]}" > "$out/bench_under_rocprof.json" 2> "$out/stats.err"
+    python3 bench.py --no-cpu-baseline --no-check --extras none "${args[@]}" > "$out/bench_under_rocprof.json" 2> "$out/stats.err"
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum \
-    --output-format csv -d "$out/rd" -o rd -- python3 bench.py --no-cpu-baseline --no-check --steps 3 --warmup 1 "${args[@]}" \
+    --output-format csv -d "$out/rd" -o rd -- python3 bench.py --no-cpu-baseline --no-check --extras none --steps 3 --warmup 1 "${args[@]}" \
     > /dev/null 2> "$out/rd.err"
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
-    --output-format csv -d "$out/wr" -o wr -- python3 bench.py --no-cpu-baseline --no-check --steps 3 --warmup 1 "${args[@]}" \
+    --output-format csv -d "$out/wr" -o wr -- python3 bench.py --no-cpu-baseline --no-check --extras none --steps 3 --warmup 1 "${args[@]}" \
     > /dev/null 2> "$out/wr.err"
 find "$out" -name "*.csv" | sort > "$out/files.txt"

@@ -14,7 +14,7 @@ for r in $(seq 1 ${ROUNDS:-1}); do
     envs=${cfg%%|*}
     args=""
     [[ "$cfg" == *"|"* ]] && args=${cfg#*|}
-    eval "env $envs timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-30} $BENCH_ARGS $args" \
+    eval "env $envs timeout -k 10 120 python bench.py --no-cpu-baseline --no-check --extras none --steps ${STEPS:-30} $BENCH_ARGS $args" \
         > gpurun_out/sw.json 2> gpurun_out/sw_err.log || exit 1
     python -c "
 import json;d=json.loads(open('gpurun_out/sw.json').read().strip().splitlines()[-1])
