@@ -139,13 +139,19 @@ def kernel_bytes_min(s, ntr=1):
 
 # ----------------------------------------------------------------------------- worker pool
 
+def _worker_init():
+    """Pool workers are single-threaded (the OpenMP field generator too): the pool is the parallelism."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+
+
 def make_pool(world):
     """Worker processes for the CPU baselines and the parity check, spawned before this process
-    touches the GPU (they never do): min(16, usable cores / ranks) per rank -- 16 is the GPU box's
-    CPU share per GPU."""
+    touches the GPU (they never do): 16 per rank (the GPU box's CPU share per GPU), fewer when the
+    cores this rank may use, shared by the node's ranks, hold less."""
     import multiprocessing
-    P = max(1, min(16, len(os.sched_getaffinity(0)) // max(world, 1)))
-    return multiprocessing.get_context("spawn").Pool(P), P
+    n = len(os.sched_getaffinity(0))
+    P = max(1, min(16, n // world if n >= 16 * world else n))
+    return multiprocessing.get_context("spawn").Pool(P, initializer=_worker_init), P
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -359,8 +365,9 @@ def _check_strip(job):
     Edges are compared by the strip of their smallest rank-owned endpoint (each local edge once)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    nx, ny, nl, full, vlimit, (R0, R1), (a, b), ntr, files = job
+    nx, ny, nl, full, vlimit, (R0, R1), (a, b), ntr, (mode, src) = job
     L = nl - 1
+    e0, e1 = strip_edge_range(nx, ny, R0, R1, a, b)
     y0, y1 = max(0, a - 1), min(ny, b + 1)
     m, _ = partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=full)
     n0, n1 = (a - y0) * nx, (b - y0) * nx        # rows [a, b) in the widened strip
@@ -370,8 +377,16 @@ def _check_strip(job):
     key = np.where(owned, ends, np.iinfo(np.int64).max).min(axis=1)
     tgt = (key >= a * nx) & (key < b * nx)
     gpu_e = partition.strip_edge_index(nx, ny, R0, R1, m.edge_gid[tgt])
+    if not np.array_equal(gpu_e, np.arange(e0, e1)):
+        raise RuntimeError(f"strip rows {a}:{b}: its edges are not the rank's edges {e0}:{e1}")
     wet = np.arange(L)[None, :] < (m.nlev_nod[n0:n1, None].astype(np.int64) - 1)
-    mm = {k: np.memmap(path, dtype=np.float64, mode="r", shape=shape) for k, (path, shape) in files.items()}
+    if mode == "files":  # the rank's whole arrays, memory-mapped: this strip's rows / edges of them
+        mm = {k: np.memmap(path, dtype=np.float64, mode="r", shape=shape) for k, (path, shape) in src.items()}
+        rows = lambda name, k, wd: mm[name][k][g0 * wd:(g0 + n1 - n0) * wd]
+        edges = lambda k: mm["adf_h"][k].reshape(-1, L)[e0:e1]
+    else:  # "data": the strip's rows / edges, sent with the job
+        rows = lambda name, k, wd: src[name][k]
+        edges = lambda k: src["adf_h"][k].reshape(-1, L)
     bad, acc = {}, [0.0, 0]
     for k in range(ntr):
         f = synth.make_fields(m, seed=43 + k)
@@ -386,16 +401,24 @@ def _check_strip(job):
         w.update(plus=p1["plus"], minus=p1["minus"])
         for name, width in OUTPUTS:
             wd = L if width == "L" else nl
-            got = mm[name][k]
             if name == "adf_h":
-                _compare(bad, name, got.reshape(-1, wd)[gpu_e], w[name].reshape(-1, wd)[tgt], acc)
+                _compare(bad, name, edges(k), w[name].reshape(-1, wd)[tgt], acc)
                 continue
-            ga = got[g0 * wd:(g0 + n1 - n0) * wd].reshape(-1, wd)
+            ga = rows(name, k, wd).reshape(-1, wd)
             wa = w[name][n0 * wd:n1 * wd].reshape(-1, wd)
             if name in ("plus", "minus"):
                 ga, wa = ga[wet], wa[wet]
             _compare(bad, name, ga, wa, acc)
     return bad, acc[0], acc[1]
+
+
+def strip_edge_range(nx, ny, R0, R1, a, b):
+    """[e0, e1): the rank's local edges (owned rows [R0, R1)) that _check_strip compares for rows
+    [a, b) -- contiguous, since an edge's smallest rank-owned endpoint lies in the row it starts in
+    (or in row R0 for the vertical/diagonal edges coming up from row R0 - 1, which lead the list)."""
+    first_of = lambda j: int(partition.strip_edge_index(nx, ny, R0, R1, [3 * nx * j])[0])
+    total = first_of(R1 - 1) + (nx if R1 - 1 == ny - 1 else 3 * nx)
+    return (0 if a == R0 else first_of(a)), (total if b == R1 else first_of(b))
 
 
 def pristine(m, name, ntr):
@@ -423,27 +446,49 @@ def verify_parallel(args, ctx, e, step, m, world, rank):
     nx, ny, nl = global_dims(args, world)
     R0, R1 = partition.strip_rows(ny, world, rank) if world > 1 else (0, ny)
     run_check_pass(args, e, step, m, ntr)
-    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    # strips of about 80k nodes (a few seconds of oracle work each), at least one per worker
+    rows = R1 - R0
+    nstrip = max(min(rows, ctx.nworkers), min(rows, -(-(rows * nx) // 80000)))
+    cuts = [R0 + (rows * s_) // nstrip for s_ in range(nstrip + 1)]
+    strips = [(cuts[s_], cuts[s_ + 1]) for s_ in range(nstrip) if cuts[s_ + 1] > cuts[s_]]
+    # the outputs reach the workers as memory-mapped files in /dev/shm when it has room for every
+    # rank's (no copy), else as the strips' slices sent with the jobs
+    need = sum(8 * max(e.size(name), 1) for name, _ in OUTPUTS)
+    shm = "/dev/shm"
+    try:
+        st_ = os.statvfs(shm)
+        use_files = st_.f_bavail * st_.f_frsize >= 1.5 * need * world
+    except OSError:
+        use_files = False
     files, paths = {}, []
     t0 = time.perf_counter()
     try:
-        for name, _ in OUTPUTS:
-            n = e.size(name)
+        if use_files:
             import tempfile
-            fd, path = tempfile.mkstemp(prefix=f"f2a_check_{os.getpid()}_{name}_", dir=shm)
-            os.close(fd)
-            paths.append(path)
-            buf = np.memmap(path, dtype=np.float64, mode="w+", shape=(max(n, 1),))
-            e.download(name, out=buf)
-            buf.flush()
-            del buf
-            files[name] = (path, (ntr, n // ntr))
-        # strips of about 80k nodes (a few seconds of oracle work each), at least one per worker
-        rows = R1 - R0
-        nstrip = max(min(rows, ctx.nworkers), min(rows, -(-(rows * nx) // 80000)))
-        cuts = [R0 + (rows * s) // nstrip for s in range(nstrip + 1)]
-        jobs = [(nx, ny, nl, not args.parity_levels, args.vlimit, (R0, R1), (cuts[s], cuts[s + 1]), ntr, files)
-                for s in range(nstrip) if cuts[s + 1] > cuts[s]]
+            for name, _ in OUTPUTS:
+                n = e.size(name)
+                fd, path = tempfile.mkstemp(prefix=f"f2a_check_{os.getpid()}_{name}_", dir=shm)
+                os.close(fd)
+                paths.append(path)
+                buf = np.memmap(path, dtype=np.float64, mode="w+", shape=(max(n, 1),))
+                e.download(name, out=buf)
+                buf.flush()
+                del buf
+                files[name] = (path, (ntr, n // ntr))
+            srcs = [("files", files)] * len(strips)
+        else:
+            host = {name: e.download(name).reshape(ntr, -1) for name, _ in OUTPUTS}
+            srcs = []
+            for a, b in strips:
+                e0, e1 = strip_edge_range(nx, ny, R0, R1, a, b)
+                d = {}
+                for name, width in OUTPUTS:
+                    wd = m.L if width == "L" else m.nl
+                    d[name] = host[name][:, e0 * wd:e1 * wd] if name == "adf_h" else \
+                        host[name][:, (a - R0) * nx * wd:(b - R0) * nx * wd]
+                srcs.append(("data", d))
+        jobs = [(nx, ny, nl, not args.parity_levels, args.vlimit, (R0, R1), st, ntr, src)
+                for st, src in zip(strips, srcs)]
         res = ctx.pool.map(_check_strip, jobs, chunksize=1)
     finally:
         for p in paths:
@@ -461,7 +506,8 @@ def verify_parallel(args, ctx, e, step, m, world, rank):
     return {"exact": not bad, "max_abs": max_abs, "mismatched_cells": bad, "cells_compared": cells,
             "tracers": ntr, "ranks": world, "oracle_s": round(t_oracle, 1),
             "against": f"oracle/fct_ale_oracle.c on {len(jobs)} row strips per rank, each widened by one ring "
-                       f"(exact without an exchange), {ctx.nworkers} worker processes per rank (per tracer)"}
+                       f"(exact without an exchange), {ctx.nworkers} worker processes per rank (per tracer); "
+                       f"outputs {'memory-mapped from /dev/shm' if use_files else 'sent with the jobs'}"}
 
 
 def reduce_check(ctx, bad, max_abs, cells):

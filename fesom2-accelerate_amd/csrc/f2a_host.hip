@@ -586,8 +586,8 @@ PlanShape plan_shape(bool batched)
     if (patch) s.patch = std::max(1, atoi(patch));  // 0 or 1: index order
     if (batched) {
         const char *gs = getenv("FESOM2_BATCH_GROUP_SHIFT");
-        if (!patch) s.patch = -1024;  // 1024 nodes where the numbering has locality (see build_plan)
-        s.gshift = gs ? atoi(gs) : -1;
+        if (!patch) s.patch = PlanShape::kAuto;
+        s.gshift = gs ? atoi(gs) : PlanShape::kAuto;
     } else {
         s.gshift = knob("FESOM2_GROUP_SHIFT", 0);  // tuning build A/B
     }
@@ -607,6 +607,14 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     d.n_edges = n_edges;
     d.nl = nl;
     d.gshift = shape.gshift;
+    if (d.gshift == PlanShape::kAuto) {
+        // half-size blocks for a batch when the halved block still keeps >= 80 % of its lanes busy:
+        // measured 6 tracers, 1.2M x 80 (40 slots, 4 columns = 160 of 192 lanes): pass -4 %;
+        // 127k x 47 (24 slots, 4 columns = 96 of 128 lanes): +2 % (batched plan)
+        const int S = p1v_slots(nl), G = p1v_group_columns(nl, 0), g2 = G / 2;
+        const int lanes = (g2 * S + 63) / 64 * 64;
+        d.gshift = (g2 >= 1 && 5 * g2 * S >= 4 * lanes) ? -1 : 0;
+    }
     const int L = nl - 1;
     char msg[256];
     auto fail = [&](const char *s) {
@@ -734,9 +742,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             }
         }
         // nodes per patch (1 = index order): the shape's (plan options FESOM2_PATCH /
-        // FESOM2_BATCH_PATCH), else by numbering; -k: k nodes for a numbering with locality
-        const int patch = shape.patch > 0 ? shape.patch
-                          : (local_numbering ? (shape.patch < 0 ? -shape.patch : 16384) : 4096);
+        // FESOM2_BATCH_PATCH), else by numbering; the batched plan's default: 4096 when its blocks
+        // are halved (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer
+        // plan's choice (127k x 47: 16384 best)
+        const int sp = shape.patch == PlanShape::kAuto ? (d.gshift < 0 ? 4096 : 0) : shape.patch;
+        const int patch = sp > 0 ? sp : (local_numbering ? 16384 : 4096);
         // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
         // tuning build
         const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);

@@ -176,8 +176,11 @@ struct Plan {
 // the patch ntracers times more tiles later -- beyond the XCD L2's lifetime with wide patches
 // (batched plan).
 struct PlanShape {
-    int patch = 0;   // nodes per BFS patch; 0: automatic (16384 / 4096 by numbering); 1: index order
-    int gshift = 0;  // MeshPlanDev::gshift
+    static constexpr int kAuto = 99;
+    int patch = 0;   // nodes per BFS patch; 0: automatic (16384 / 4096 by numbering); 1: index order;
+                     // kAuto (batched): 4096 where the blocks are halved, else automatic
+    int gshift = 0;  // MeshPlanDev::gshift; kAuto: half-size blocks where they keep >= 80 % of the
+                     // block's lanes busy (build_plan)
 };
 // the shape of the single-tracer (batched = false) or the batched plan, with the plan options
 // FESOM2_PATCH / FESOM2_BATCH_PATCH and FESOM2_BATCH_GROUP_SHIFT (read when the plan is built)

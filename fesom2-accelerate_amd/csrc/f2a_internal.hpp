@@ -196,8 +196,9 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // sequence's fast mode (no area/hnode/hnode_new/del_v needed)
 hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // columns per p1v block for nl levels (the shape launch_p1v uses; the plan's int_G) at the plan's
-// group shift
+// group shift, and its slots (threads) per column
 int p1v_group_columns(int nl, int shift);
+int p1v_slots(int nl);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);
 constexpr int kMaxInternal = 64;  // most block-internal edges a p1v block limits (LDS staging)

@@ -1304,6 +1304,12 @@ hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s
 #endif
 }
 
+int p1v_slots(int nl)
+{
+    const int L = nl - 1;
+    return odd_pairs(L) ? (L + 1) / 2 : L / levels_per_thread(L);
+}
+
 int p1v_group_columns(int nl, int shift)
 {
     const int L = nl - 1;

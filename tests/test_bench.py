@@ -161,8 +161,9 @@ def _rank_outputs(g, m, ntr):
     return {k: np.stack(v) for k, v in out.items()}
 
 
+@pytest.mark.parametrize("mode", ["files", "data"])
 @pytest.mark.parametrize("world,ntr,full", [(1, 1, False), (2, 2, False), (3, 1, True)])
-def test_parallel_strip_check_is_exact_and_counts_each_cell_once(tmp_path, world, ntr, full):
+def test_parallel_strip_check_is_exact_and_counts_each_cell_once(tmp_path, world, ntr, full, mode):
     """bench.py's parallel check: the oracle on row strips widened by one ring equals the
     single-domain pass on the strip's rows and edges (no exchange), every local edge is compared by
     exactly one strip, and a changed cell is reported once."""
@@ -184,8 +185,19 @@ def test_parallel_strip_check_is_exact_and_counts_each_cell_once(tmp_path, world
                 mm.flush()
                 files[name] = (str(p), a.shape)
             cuts = [R0, R0 + (R1 - R0) // 3, R0 + 2 * (R1 - R0) // 3, R1]
-            res = [bench._check_strip((nx, ny, nl, full, 1, (R0, R1), (cuts[k], cuts[k + 1]), ntr, files))
-                   for k in range(3) if cuts[k + 1] > cuts[k]]
+            res = []
+            for k in range(3):
+                a_, b_ = cuts[k], cuts[k + 1]
+                if b_ <= a_:
+                    continue
+                if mode == "files":
+                    src = files
+                else:  # the strip's slices, as verify_parallel sends them without /dev/shm room
+                    e0, e1 = bench.strip_edge_range(nx, ny, R0, R1, a_, b_)
+                    src = {name: (arr[:, e0 * g.L:e1 * g.L] if name == "adf_h" else
+                                  arr[:, (a_ - R0) * nx * (g.L if w == "L" else nl):(b_ - R0) * nx * (g.L if w == "L" else nl)])
+                           for (name, w), arr in zip(bench.OUTPUTS, [arrs[n] for n, _ in bench.OUTPUTS])}
+                res.append(bench._check_strip((nx, ny, nl, full, 1, (R0, R1), (a_, b_), ntr, (mode, src))))
             bad, cells = {}, 0
             for b_, _, c in res:
                 for k_, v in b_.items():
