@@ -983,7 +983,8 @@ def main():
                     help="the strong-scaling leg's global mesh (BASELINE configs[4]: 9.6M x 80)")
     ap.add_argument("--comm-timeout", type=float, default=180.0,
                     help="watchdog bound (s) of RCCL communicator setup and of the first exchange step")
-    ap.add_argument("--leg-timeout", type=float, default=900.0, help="watchdog bound (s) of each extra leg")
+    ap.add_argument("--leg-timeout", type=float, default=420.0,
+                    help="watchdog bound (s) of each extra leg (the 9.6M x 80 leg on one GPU takes about 60 s)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
     args = ap.parse_args()
@@ -1089,7 +1090,21 @@ def main():
             la.traffic = os.path.join(ROOT, "profiles", "none.json")  # the per-config traffic files below
             ctx.watchdog.arm(f"extra leg {name}", args.leg_timeout)
             t0 = time.perf_counter()
-            rec = run_leg(la, ctx)
+            try:
+                rec = run_leg(la, ctx)
+            except Exception as ex:  # an extra leg must not cost the measured headline its line
+                ctx.watchdog.disarm()
+                log(f"rank {rank}: extra leg {name} failed: {type(ex).__name__}: {ex}")
+                out["extra"][name] = {"error": f"{type(ex).__name__}: {ex}"}
+                exact = False
+                if world > 1:
+                    # the other ranks may wait in a collective of this leg: end the run here (their
+                    # gloo calls fail once this rank is gone); rank 0 reports what was measured
+                    if rank == 0:
+                        print(json.dumps(out), flush=True)
+                    sys.stderr.flush()
+                    os._exit(4)
+                continue
             ctx.watchdog.disarm()
             out["extra"][name] = compact(rec, la, world)
             out["extra"][name]["leg_s"] = round(time.perf_counter() - t0, 1)

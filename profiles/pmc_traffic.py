@@ -12,7 +12,7 @@ TCC_EA0_WRREQ_64B_sum = 24.0e6 (x 64 B = 1.536 GB).  So
 
 (the counters include Infinity-Cache hits: this is L2-miss traffic, an upper bound on HBM bytes).
 
-usage: pmc_traffic.py READ_CSV WRITE_CSV WORKLOAD OUT_JSON
+usage: pmc_traffic.py READ_CSV WRITE_CSV WORKLOAD OUT_JSON [TRACERS [SOURCE]]
 """
 import collections
 import csv
@@ -44,6 +44,8 @@ def per_kernel(path):
 
 def main():
     rd, wr, workload, out = sys.argv[1:5]
+    tracers = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    source = sys.argv[6] if len(sys.argv) > 6 else ""
     R, W = per_kernel(rd), per_kernel(wr)
     res = {}
     for k, name in NAMES.items():
@@ -55,8 +57,9 @@ def main():
         wb = 64 * w.get("TCC_EA0_WRREQ_64B_sum", 0) + 32 * (w.get("TCC_EA0_WRREQ_sum", 0) -
                                                             w.get("TCC_EA0_WRREQ_64B_sum", 0))
         res[name] = {"read_bytes": int(rb), "write_bytes": int(wb), "total": int(rb + wb)}
-    doc = {"workload": workload, "bytes_per_launch": {k: v["total"] for k, v in res.items()}, "detail": res,
-           "method": __doc__.strip().splitlines()[0] + " -- see profiles/pmc_traffic.py"}
+    doc = {"workload": workload, "tracers": tracers, "bytes_per_launch": {k: v["total"] for k, v in res.items()},
+           "detail": res, "method": __doc__.strip().splitlines()[0] + " -- see profiles/pmc_traffic.py",
+           "source": source}
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc, indent=1))
 
