@@ -576,6 +576,11 @@ __device__ __forceinline__ void p2_node_work(const MeshPlanDev &mp, P2Args &a, c
 // ---- host-side launch utilities
 static inline unsigned threads_for(int G, int S) { return (unsigned)(((G * S + kWave - 1) / kWave) * kWave); }
 
+// columns per block of a plan's column-group kernels for S slots per column: the plan's explicit
+// count (MeshPlanDev::gcols, validated against the widest column shape) or group_columns' natural
+// one times 2^gshift
+static inline int plan_columns(int S, const MeshPlanDev &mp) { return mp.gcols > 0 ? mp.gcols : group_columns(S, mp.gshift); }
+
 // odd L in level pairs (the last slot of a column holds one level; FESOM2_ODD_PAIR=0 in the tuning
 // build: one level per thread)
 static inline bool odd_pairs(int L) { return L % 2 == 1 && L >= 3 && knob("FESOM2_ODD_PAIR", 1) != 0; }

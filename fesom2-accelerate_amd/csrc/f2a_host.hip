@@ -441,7 +441,12 @@ void timing_begin(const char *name, hipStream_t s, void **token)
 {
     auto *t = new TimedLaunch;
     t->name = name;
-    if (hipEventCreate(&t->start) != hipSuccess || hipEventCreate(&t->stop) != hipSuccess) {
+    // device-scope release: the default system-scope release writes back and invalidates the L2 at
+    // every event, which slows the next kernel and stretches the gap between launches (the events
+    // only time kernels; the host reads them after hipEventSynchronize).  Tuning build A/B:
+    // FESOM2_EVENT_FENCE=1 restores the default fence.
+    const unsigned flags = knob("FESOM2_EVENT_FENCE", 0) ? hipEventDefault : hipEventReleaseToDevice;
+    if (hipEventCreateWithFlags(&t->start, flags) != hipSuccess || hipEventCreateWithFlags(&t->stop, flags) != hipSuccess) {
         if (t->start) (void)hipEventDestroy(t->start);
         delete t;
         *token = nullptr;
@@ -586,10 +591,13 @@ PlanShape plan_shape(bool batched)
     if (patch) s.patch = std::max(1, atoi(patch));  // 0 or 1: index order
     if (batched) {
         const char *gs = getenv("FESOM2_BATCH_GROUP_SHIFT");
+        const char *gc = getenv("FESOM2_BATCH_GROUP");
         if (!patch) s.patch = PlanShape::kAuto;
         s.gshift = gs ? atoi(gs) : PlanShape::kAuto;
+        s.gcols = gc ? std::max(0, atoi(gc)) : 0;
     } else {
         s.gshift = knob("FESOM2_GROUP_SHIFT", 0);  // tuning build A/B
+        s.gcols = knob("FESOM2_GROUP", 0);
     }
     return s;
 }
@@ -607,6 +615,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     d.n_edges = n_edges;
     d.nl = nl;
     d.gshift = shape.gshift;
+    // explicit columns per block: every column-group kernel must fit 1024 threads with its widest
+    // shape (one level per thread: nl - 1 slots)
+    d.gcols = (shape.gcols > 0 && shape.gcols * (nl - 1) <= 1024) ? shape.gcols : 0;
+    if (d.gcols) d.gshift = 0;
     if (d.gshift == PlanShape::kAuto) {
         // half-size blocks for a batch when the halved block still keeps >= 80 % of its lanes busy:
         // measured 6 tracers, 1.2M x 80 (40 slots, 4 columns = 160 of 192 lanes): pass -4 %;
@@ -745,7 +757,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // FESOM2_BATCH_PATCH), else by numbering; the batched plan's default: 4096 when its blocks
         // are halved (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer
         // plan's choice (127k x 47: 16384 best)
-        const int sp = shape.patch == PlanShape::kAuto ? (d.gshift < 0 ? 4096 : 0) : shape.patch;
+        const int sp = shape.patch == PlanShape::kAuto ? (d.gshift < 0 || d.gcols ? 4096 : 0) : shape.patch;
         const int patch = sp > 0 ? sp : (local_numbering ? 16384 : 4096);
         // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
         // tuning build
@@ -864,7 +876,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
         const char *ienv = getenv("FESOM2_P1V_B3H");
         if (ienv ? atoi(ienv) != 0 : wet_cells >= (32ll << 20)) {
-            const int IG = p1v_group_columns(nl, d.gshift);
+            const int IG = p1v_group_columns(nl, d.gshift, d.gcols);
             std::vector<int> pos(n_owned);
             for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
             auto internal = [&](const int4 &ei) { return pos[ei.x] / IG == pos[ei.y] / IG; };

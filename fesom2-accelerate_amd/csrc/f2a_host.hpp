@@ -181,6 +181,7 @@ struct PlanShape {
                      // kAuto (batched): 4096 where the blocks are halved, else automatic
     int gshift = 0;  // MeshPlanDev::gshift; kAuto: half-size blocks where they keep >= 80 % of the
                      // block's lanes busy (build_plan)
+    int gcols = 0;   // MeshPlanDev::gcols: columns per block (> 0 overrides gshift)
 };
 // the shape of the single-tracer (batched = false) or the batched plan, with the plan options
 // FESOM2_PATCH / FESOM2_BATCH_PATCH and FESOM2_BATCH_GROUP_SHIFT (read when the plan is built)

@@ -116,8 +116,9 @@ static_assert(sizeof(NodeRec) == 192, "NodeRec layout");
 struct MeshPlanDev {
     int n_owned = 0;       // myDim_nod2D
     // block size of the column-group kernels: 2^gshift times group_columns' natural G (the batched
-    // plan halves it, see get_plan)
+    // plan halves it, see get_plan), or exactly gcols columns when > 0
     int gshift = 0;
+    int gcols = 0;
     int n_total = 0;       // myDim_nod2D + eDim_nod2D
     int n_edges = 0;       // myDim_edge2D
     int nl = 0;
@@ -197,7 +198,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s);
 // columns per p1v block for nl levels (the shape launch_p1v uses; the plan's int_G) at the plan's
 // group shift, and its slots (threads) per column
-int p1v_group_columns(int nl, int shift);
+int p1v_group_columns(int nl, int shift, int cols = 0);
 int p1v_slots(int nl);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);

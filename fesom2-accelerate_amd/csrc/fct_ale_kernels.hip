@@ -1273,12 +1273,12 @@ static hipError_t p1_launch_tuning(const MeshPlanDev &mp, const P1Args &a, hipSt
 hipError_t launch_p1_fused(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 {
     if (odd_pairs(a.nl - 1) && a.vlimit == 1) {
-        const int L = a.nl - 1, S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int L = a.nl - 1, S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = 2 * (size_t)G * L * sizeof(real) + (size_t)G * sizeof(NodeRec);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, false, 4, true>), groups, G, S, lds, s, mp, a, G, 1.0f / (float)S);
     }
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
 #if F2A_TUNING
     // other gather batches (FESOM2_P1_BATCH = 10*RB + EB), cache policies
@@ -1310,8 +1310,9 @@ int p1v_slots(int nl)
     return odd_pairs(L) ? (L + 1) / 2 : L / levels_per_thread(L);
 }
 
-int p1v_group_columns(int nl, int shift)
+int p1v_group_columns(int nl, int shift, int cols)
 {
+    if (cols > 0) return cols;
     const int L = nl - 1;
     if (odd_pairs(L)) return group_columns((L + 1) / 2, shift);
     return group_columns(L / levels_per_thread(L), shift);
@@ -1321,7 +1322,7 @@ int p1v_group_columns(int nl, int shift)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a)
 {
     return mp.int_G > 0 && mp.int_ptr && mp.int_edges && a.vlimit >= 1 && a.vlimit <= 3 &&
-           knob("FESOM2_P1V_B3H", 1) != 0 && p1v_group_columns(a.nl, mp.gshift) == mp.int_G;
+           knob("FESOM2_P1V_B3H", 1) != 0 && p1v_group_columns(a.nl, mp.gshift, mp.gcols) == mp.int_G;
 }
 
 
@@ -1331,7 +1332,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
 {
     const int L = a.nl - 1;
     if (odd_pairs(L) && a.vlimit != 1) {  // the product's forms (p1v_launch_G: pairs at every vlimit)
-        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1343,7 +1344,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
         F2A_LAUNCH_GROUPS((k_p1<3, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
     }
     if (odd_pairs(L) && a.vlimit == 1) {
-        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, 1, in);
         const float inv = 1.0f / (float)S;
@@ -1356,7 +1357,7 @@ static hipError_t launch_p1v_tuning(const MeshPlanDev &mp, const P1Args &a, hipS
         if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 20, true>), groups, G, S, lds, s, mp, a, G, inv);
         F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, false, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1409,7 +1410,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         const int L = a.nl - 1;
         const bool odd = odd_pairs(L);
         if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+            const int S = (L + 1) / 2, G = plan_columns(S, mp);
             const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
             const size_t lds = p1_lds_bytes(G, L, 1, in);
             const float inv = 1.0f / (float)S;
@@ -1433,7 +1434,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
         const int L = a.nl - 1;
         const bool odd = odd_pairs(L);
         if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+            const int S = (L + 1) / 2, G = plan_columns(S, mp);
             const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
             const size_t lds = p1_lds_bytes(G, L, 1, in);
             const float inv = 1.0f / (float)S;
@@ -1457,7 +1458,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     // b3-horizontal, +32 their entries staged into LDS by DMA.  NT: the single-use streams
     // (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
     if (odd_pairs(L)) {  // odd L in level pairs, every vlimit (the 3-point bounds of vlimit 2/3 skip the pad level)
-        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1473,7 +1474,7 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4, true>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1512,7 +1513,7 @@ hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const bool in = p1v_limits_internal(mp, a);
     const int L = a.nl - 1;
     if (odd_pairs(L)) {
-        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
         const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
         const float inv = 1.0f / (float)S;
@@ -1528,7 +1529,7 @@ hipError_t launch_p1_b3v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 64, true>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = p1_lds_bytes(G, L, a.vlimit, in);
@@ -1565,7 +1566,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const bool NT = (knob("FESOM2_NT", 6) & 2) != 0;
     const bool pair = knob("FESOM2_NL_PAIR", 1) != 0;
     if (odd_pairs(L)) {
-        const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.count + G - 1) / G * a.tr.n;
         const size_t lds = (size_t)G * sizeof(NodeRec);
         const float invS = 1.0f / (float)S;
@@ -1576,7 +1577,7 @@ hipError_t launch_p2h(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
 #endif
         F2A_LAUNCH_GROUPS((k_p2h<2, 4, true, true, true>), groups, G, S, lds, s, mp, a, G, invS);
     }
-    const int C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1604,7 +1605,7 @@ hipError_t launch_p2_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s
     const int L = a.nl - 1;
     // levels per thread of the node kernel: FESOM2_P2_CPT (tuning build; default as the other kernels)
     const int C = (L % 2 == 0 && knob("FESOM2_P2_CPT", levels_per_thread(L)) == 2) ? 2 : 1;
-    const int S = L / C, G = group_columns(S, mp.gshift);
+    const int S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1643,7 +1644,7 @@ hipError_t launch_c_fused(const MeshPlanDev &mp, const P2Args &a, hipStream_t s)
     const int L = a.nl - 1;
     const bool odd = L % 2 == 1;
     if (odd && L < 3) return hipErrorInvalidValue;
-    const int S = (L + 1) / 2, G = group_columns(S, mp.gshift);
+    const int S = (L + 1) / 2, G = plan_columns(S, mp);
     const long groups = (a.count + G - 1) / G;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1787,7 +1788,7 @@ hipError_t launch_b3h_edges(const int4 *ei, int count, int nl, const real *plus,
 
 hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_t s)
 {
-    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int L = a.nl - 1, C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(a.count + G - 1) / G * a.tr.n;
     const float invS = 1.0f / (float)S;
     const size_t lds = (size_t)G * sizeof(NodeRec);
@@ -1798,7 +1799,7 @@ hipError_t launch_p2_iter(const MeshPlanDev &mp, const P2IterArgs &a, hipStream_
 hipError_t launch_b3h_iter(const MeshPlanDev &mp, int nl, const real *plus, const real *minus, real *adf_h,
                            real *adf_h2, const Tracers &tr, hipStream_t s)
 {
-    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = group_columns(S, mp.gshift);
+    const int L = nl - 1, C = levels_per_thread(L), S = L / C, G = plan_columns(S, mp);
     const long groups = (long)(mp.n_edges + G - 1) / G * tr.n;
     const float invS = 1.0f / (float)S;
     if (C == 2)

@@ -246,7 +246,8 @@ def test_split_by_direction_partitioned_overlap(comm, internal, nl, monkeypatch)
 
 @pytest.mark.parametrize("shape", [{}, {"FESOM2_BATCH_GROUP_SHIFT": "0"},
                                    {"FESOM2_BATCH_GROUP_SHIFT": "-2", "FESOM2_BATCH_PATCH": "64"},
-                                   {"FESOM2_BATCH_PATCH": "1"}],
+                                   {"FESOM2_BATCH_PATCH": "1"}, {"FESOM2_BATCH_GROUP": "6"},
+                                   {"FESOM2_BATCH_GROUP": "5", "FESOM2_BATCH_PATCH": "300"}],
                          ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()) or "default")
 @pytest.mark.parametrize("name,full", [("8k x 20", False), ("127k x 47", True)])
 @pytest.mark.parametrize("internal", ["0", "1"])
@@ -266,9 +267,11 @@ def test_batched_plan_shapes(shape, name, full, internal, monkeypatch):
         one, many = dm.info(), dm.info(batched=True)
         if internal == "1" and many["p1v_columns"]:  # (0: some block has too many internal edges)
             # default: half-size blocks where they keep >= 80 % of the lanes busy (20 levels: 160 of
-            # 192 lanes; 47 levels in pairs: 96 of 128, so not)
+            # 192 lanes; 47 levels in pairs: 96 of 128, so not); FESOM2_BATCH_GROUP: exactly that many
             shift = int(shape.get("FESOM2_BATCH_GROUP_SHIFT", "-1" if name == "8k x 20" else "0"))
-            assert many["p1v_columns"] * 2 ** -shift == one["p1v_columns"], (one, many)
+            want = int(shape["FESOM2_BATCH_GROUP"]) if "FESOM2_BATCH_GROUP" in shape else \
+                one["p1v_columns"] // 2 ** -shift
+            assert many["p1v_columns"] == want, (one, many)
         assert e.pre_comm_v() == 7, abi.last_error()
         assert e.post_comm_h() == 9, abi.last_error()
         e.sync()
