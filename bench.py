@@ -725,17 +725,21 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         abi.device_sync()
 
     # ---- timed region: exactly K steps, barrier + device sync on both sides
-    abi.kernel_timing(not args.graph and args.kernel_timing != "none")
+    timing = not args.graph and args.kernel_timing != "none"
     # the split pass's dominant kernel is p1v (an iterated FCT call is dominated by its iteration kernels)
     timed_only = args.kernel_timing == "dominant" and args.path == "split" and args.fct_iter == 1 and not args.graph
     abi.kernel_timing_only("fct_ale_p1v" if timed_only else None)
     abi.kernel_timing_reset()
+    # the dominant kernel's events on every --timing-every'th step of the timed region (a sample:
+    # each event pair costs a small partition's pass ~2 %; switching does not synchronise)
+    every = max(1, args.timing_every) if timed_only else 1
     ctx.barrier()
     abi.device_sync()
     ev0, ev1 = abi.Event(), abi.Event()
     ev0.record(stream)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        abi.kernel_timing(timing and i % every == 0)
         step()
     ev1.record(stream)
     abi.device_sync()
@@ -970,6 +974,9 @@ def main():
                          "(no roofline).  Each timed launch adds two events to the stream: at 127k x 47 timing "
                          "every launch costs 5 %% of the pass.  With 'dominant' the other kernels are timed on "
                          "a few extra steps after the timed region")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="with --kernel-timing dominant: bracket the dominant kernel of every k-th timed step "
+                         "(a sample of K/k launches; 1: every step)")
     ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity check")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "host"],
                     help="N > 1 halo of fct_plus/fct_minus: in-library RCCL (the benchmark), or host copies "

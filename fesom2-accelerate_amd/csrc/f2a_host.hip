@@ -441,11 +441,11 @@ void timing_begin(const char *name, hipStream_t s, void **token)
 {
     auto *t = new TimedLaunch;
     t->name = name;
-    // device-scope release: the default system-scope release writes back and invalidates the L2 at
-    // every event, which slows the next kernel and stretches the gap between launches (the events
-    // only time kernels; the host reads them after hipEventSynchronize).  Tuning build A/B:
-    // FESOM2_EVENT_FENCE=1 restores the default fence.
-    const unsigned flags = knob("FESOM2_EVENT_FENCE", 0) ? hipEventDefault : hipEventReleaseToDevice;
+    // default (system-scope) release.  Measured against a device-scope release
+    // (hipEventReleaseToDevice, tuning build FESOM2_EVENT_FENCE=0): 127k x 47 the same within noise,
+    // 1.2M x 80 1 % slower per pass with the device-scope events around p1v (profiles/r04/
+    // r04f_sweep_eventfence_*.txt), so the default stays.
+    const unsigned flags = knob("FESOM2_EVENT_FENCE", 1) ? hipEventDefault : hipEventReleaseToDevice;
     if (hipEventCreateWithFlags(&t->start, flags) != hipSuccess || hipEventCreateWithFlags(&t->stop, flags) != hipSuccess) {
         if (t->start) (void)hipEventDestroy(t->start);
         delete t;
@@ -469,10 +469,10 @@ void timing_end(void *token, hipStream_t s)
 
 extern "C" {
 
+// Switching only flips the flag: the recorded events are resolved when the statistics are read (or
+// reset), so a caller may time every k-th step without a host synchronisation in between.
 void fesom2_kernel_timing_(int *on)
 {
-    std::lock_guard<std::mutex> lock(f2a::g_tmutex);
-    f2a::resolve_pending();
     f2a::g_timing = on && *on;
 }
 
@@ -619,13 +619,25 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     // shape (one level per thread: nl - 1 slots)
     d.gcols = (shape.gcols > 0 && shape.gcols * (nl - 1) <= 1024) ? shape.gcols : 0;
     if (d.gcols) d.gshift = 0;
+    long long wet_cells = 0;  // owned wet cells (the size rules below and FESOM2_P1V_B3H)
+    if (m.nlev_nod)
+        for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
     if (d.gshift == PlanShape::kAuto) {
-        // half-size blocks for a batch when the halved block still keeps >= 80 % of its lanes busy:
-        // measured 6 tracers, 1.2M x 80 (40 slots, 4 columns = 160 of 192 lanes): pass -4 %;
-        // 127k x 47 (24 slots, 4 columns = 96 of 128 lanes): +2 % (batched plan)
-        const int S = p1v_slots(nl), G = p1v_group_columns(nl, 0), g2 = G / 2;
-        const int lanes = (g2 * S + 63) / 64 * 64;
-        d.gshift = (g2 >= 1 && 5 * g2 * S >= 4 * lanes) ? -1 : 0;
+        // a batch on a large partition (>= 32M owned wet cells): smaller blocks -- the largest column
+        // count below the natural one that keeps >= 90 % of the block's lanes busy.  Measured, 6
+        // tracers at 1.2M x 80 (40 slots; 8 columns natural), one box, 3 interleaved rounds:
+        // 6 columns (240 of 256 lanes) 21.26 ms, 3: 21.52-21.67, 12: 21.65, 4: 21.76, 7: 23.15,
+        // 8 (the single plan): 23.0-23.3.  On 127k x 47 (6M cells) every smaller block loses
+        // (5 columns: +1.6 %, 7: +0.6 %), so small partitions keep the single plan's shape.
+        d.gshift = 0;
+        if (wet_cells >= (32ll << 20)) {
+            const int S = p1v_slots(nl), Gn = p1v_group_columns(nl, 0);
+            for (int g = Gn - 1; g >= 1; g--)
+                if (10 * g * S >= 9 * ((g * S + 63) / 64 * 64) && g * (nl - 1) <= 1024) {
+                    d.gcols = g;
+                    break;
+                }
+        }
     }
     const int L = nl - 1;
     char msg[256];
@@ -755,7 +767,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         }
         // nodes per patch (1 = index order): the shape's (plan options FESOM2_PATCH /
         // FESOM2_BATCH_PATCH), else by numbering; the batched plan's default: 4096 when its blocks
-        // are halved (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer
+        // are smaller (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer
         // plan's choice (127k x 47: 16384 best)
         const int sp = shape.patch == PlanShape::kAuto ? (d.gshift < 0 || d.gcols ? 4096 : 0) : shape.patch;
         const int patch = sp > 0 ? sp : (local_numbering ? 16384 : 4096);
@@ -872,8 +884,6 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         d.n_edge_interior = (int)std::count_if(einfo.begin(), einfo.end(), interior_edge);
         // FESOM2_P1V_B3H: 1 on, 0 off, unset: on from 32M owned wet cells per GPU -- measured
         // 1.2M x 80 (96M cells) -3.5 % per pass, 127k x 47 (6M cells, latency-bound) +2 %
-        long long wet_cells = 0;
-        for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
         const char *ienv = getenv("FESOM2_P1V_B3H");
         if (ienv ? atoi(ienv) != 0 : wet_cells >= (32ll << 20)) {
             const int IG = p1v_group_columns(nl, d.gshift, d.gcols);

@@ -171,16 +171,16 @@ struct Plan {
 
 // Processing-order options of a plan.  Single-tracer calls use the defaults (16384-node patches
 // for a numbering with locality, the natural block size); calls with ntracers > 1 get a plan of
-// their own (get_plan(..., batched)): 1024-node patches and half-size blocks, because a batch's
+// their own (get_plan(..., batched)): on large partitions 4096-node patches and smaller blocks, because a batch's
 // tiles run (column group, tracer) tracer-fastest, which puts a column's reuse by the next row of
 // the patch ntracers times more tiles later -- beyond the XCD L2's lifetime with wide patches
 // (batched plan).
 struct PlanShape {
     static constexpr int kAuto = 99;
     int patch = 0;   // nodes per BFS patch; 0: automatic (16384 / 4096 by numbering); 1: index order;
-                     // kAuto (batched): 4096 where the blocks are halved, else automatic
-    int gshift = 0;  // MeshPlanDev::gshift; kAuto: half-size blocks where they keep >= 80 % of the
-                     // block's lanes busy (build_plan)
+                     // kAuto (batched): 4096 where the blocks are smaller, else automatic
+    int gshift = 0;  // MeshPlanDev::gshift; kAuto (batched): on partitions of >= 32M wet cells the
+                     // largest column count below the natural one with >= 90 % of the lanes busy
     int gcols = 0;   // MeshPlanDev::gcols: columns per block (> 0 overrides gshift)
 };
 // the shape of the single-tracer (batched = false) or the batched plan, with the plan options

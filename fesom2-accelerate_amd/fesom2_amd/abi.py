@@ -35,6 +35,10 @@ EXPORTS = (
     "fesom2_graph_info_", "fesom2_mesh_info_", "fesom2_bind_c_vertical_",
 )
 
+# the reference's C++ convenience entries (include/fesom2-accelerate-legacy.hpp: C linkage, plain
+# values, `struct gpuMemory *` = the handle's void*, a hipStream_t stream)
+LEGACY_EXPORTS = ("fct_ale_a1_accelerated", "fct_ale_a2_accelerated", "fct_ale_a1_a2_accelerated")
+
 _dll = None
 
 
@@ -66,6 +70,18 @@ def arr(a):
     """host array argument (numpy, contiguous)."""
     assert a.flags.c_contiguous, "host arrays must be contiguous"
     return a.ctypes.data_as(C.c_void_p)
+
+
+def legacy():
+    """The engine library with the argument types of the legacy C++ entries set."""
+    lib = dll()
+    vp, i, b = C.c_void_p, C.c_int, C.c_bool
+    lib.fct_ale_a1_accelerated.argtypes = [i, i, vp, vp, vp, vp, vp, b, vp]
+    lib.fct_ale_a2_accelerated.argtypes = [i, i, vp, vp, vp, vp, vp, b, vp]
+    lib.fct_ale_a1_a2_accelerated.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, b, vp]
+    for name in LEGACY_EXPORTS:
+        getattr(lib, name).restype = None
+    return lib
 
 
 def last_error():

@@ -188,8 +188,9 @@ void fesom2_free_pinned_(void **hostptr);
 void fesom2_device_sync_(int *istat);
 const char *fesom2_last_error(void);
 /* Per-kernel timing: while enabled, every launch is bracketed by HIP events on its stream.
- * fesom2_kernel_stats_ writes "name count total_ms" lines (NUL-terminated, truncated to *len bytes)
- * and sets *len to the size needed. */
+ * Switching it on or off does not synchronise (the events are resolved when the statistics are read
+ * or reset), so a harness may time a sample of the steps.  fesom2_kernel_stats_ writes "name count
+ * total_ms" lines (NUL-terminated, truncated to *len bytes) and sets *len to the size needed. */
 void fesom2_kernel_timing_(int *on);
 /* Restrict the timing to launches named `name` (NULL or "": every launch).  Each timed launch adds
  * two events on its stream; timing one kernel keeps the others' boundaries free of them. */

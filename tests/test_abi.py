@@ -89,3 +89,14 @@ def test_tuning_build_exports_the_same_abi():
         pytest.skip("tuning build not made")
     out = subprocess.run(["nm", "-D", "--defined-only", tuning], capture_output=True, text=True, check=True).stdout
     assert set(header_functions()) <= {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+def test_legacy_cpp_entries_are_declared_and_exported():
+    """The reference's C++ convenience entries (reference include/fesom2-accelerate.h:155-209) are
+    declared in include/fesom2-accelerate-legacy.hpp with C linkage and exported."""
+    txt = open(os.path.join(REPO_ROOT, "include", "fesom2-accelerate-legacy.hpp")).read()
+    declared = set(re.findall(r"^void\s+([A-Za-z0-9_]+)\s*\(", txt, flags=re.M))
+    assert declared == set(abi.LEGACY_EXPORTS)
+    assert declared <= exported_symbols()
+    assert 'extern "C"' in txt and "hipStream_t stream = nullptr" in txt
+

@@ -266,9 +266,9 @@ def test_batched_plan_shapes(shape, name, full, internal, monkeypatch):
     try:
         one, many = dm.info(), dm.info(batched=True)
         if internal == "1" and many["p1v_columns"]:  # (0: some block has too many internal edges)
-            # default: half-size blocks where they keep >= 80 % of the lanes busy (20 levels: 160 of
-            # 192 lanes; 47 levels in pairs: 96 of 128, so not); FESOM2_BATCH_GROUP: exactly that many
-            shift = int(shape.get("FESOM2_BATCH_GROUP_SHIFT", "-1" if name == "8k x 20" else "0"))
+            # default on these small partitions: the single plan's blocks (smaller ones only from 32M
+            # wet cells, test_batched_plan_of_a_large_partition); FESOM2_BATCH_GROUP: exactly that many
+            shift = int(shape.get("FESOM2_BATCH_GROUP_SHIFT", "0"))
             want = int(shape["FESOM2_BATCH_GROUP"]) if "FESOM2_BATCH_GROUP" in shape else \
                 one["p1v_columns"] // 2 ** -shift
             assert many["p1v_columns"] == want, (one, many)
@@ -287,3 +287,17 @@ def test_batched_plan_shapes(shape, name, full, internal, monkeypatch):
     finally:
         e.free()
         dm.free()
+
+
+def test_batched_plan_of_a_large_partition():
+    """From 32M owned wet cells the batched plan takes the largest column count below the natural
+    one that keeps >= 90 % of a block's lanes busy: 1.2M x 80 (40 slots per column, 8 columns
+    natural) -> 6 columns (240 of 256 lanes); the single-tracer plan keeps 8."""
+    m = synth.config_mesh("1.2M x 80", full_depth=True)
+    dm = engine.DeviceMesh(m)
+    try:
+        assert dm.info()["p1v_columns"] == 8
+        assert dm.info(batched=True)["p1v_columns"] == 6
+    finally:
+        dm.free()
+
