@@ -8,8 +8,9 @@
 //   cols   the same in p1v's block shape: G = 8 columns x L/2 threads, XCD-swizzled tiles, the three
 //          stride-nl arrays at nl = L+1 (8-byte aligned 16-B loads), adf_h as three columns per node
 // Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe tools/stream_probe.hip (build() does)
-// Run:   ./stream_probe [nodes=1200000] [L=80] [--json]   (--json: one line with the copy and the
-//        G = 8 column-pattern rates, which bench.py reports beside the roofline)
+// Run:   ./stream_probe [nodes=1200000] [L=80] [--json|--text] [tracers]  (--json: one line with the copy
+//        and the G = 8 column-pattern rates, which bench.py reports beside the roofline; tracers > 1
+//        adds the batched pattern, one line per block shape and tile order)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -137,11 +138,43 @@ __global__ __launch_bounds__(1024) void k_cols_odd(Arrays a, int nodes, int L, i
     st(a.adfv_o + ab, s - h);
 }
 
+// batched tracers (fct_ale_pre_comm_v_acc_ with ntracers > 1): T tracers' own arrays (ttf, LO,
+// adf_v, del_v, 3 x adf_h read; plus, minus, adf_v, del_v written) tracer k at offset k * tstride, the
+// mesh fields (area_inv, area at stride nl; hnode, hnode_new) shared; tile -> (column group,
+// tracer), tracer fastest (the product's p1v order) or slowest (major = 1)
+__global__ __launch_bounds__(1024) void k_cols_batch(Arrays a, int nodes, int L, int G, int T, size_t tstride,
+                                                     int major)
+{
+    const int S = L / 2, t = threadIdx.x, j = t / S, u = t - j * S;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    int g, tr;
+    if (major) {
+        const int groups = gridDim.x / T;
+        tr = tile / groups;
+        g = tile - tr * groups;
+    } else {
+        g = tile / T;
+        tr = tile - g * T;
+    }
+    const int n = g * G + j;
+    if (j >= G || n >= nodes) return;
+    const int z0 = 2 * u, nl = L + 1;
+    const size_t o = (size_t)tr * tstride, b = (size_t)n * L + z0, ab = (size_t)n * nl + z0;
+    d2 s = ld(a.ttf + o + b) + ld(a.LO + o + b) + ld(a.adfv + o + ab) + ld(a.ainv + ab) + ld(a.area + ab) +
+           ld(a.hn + b) + ld(a.hnn + b) + ld(a.dv + o + b);
+    const size_t e = o * 3 + (size_t)3 * n * L + z0;
+    d2 h = ld(a.adfh + e) + ld(a.adfh + e + L) + ld(a.adfh + e + 2 * L);
+    st(a.plus + o + b, s);
+    st(a.minus + o + b, h);
+    st(a.adfv_o + o + ab, s - h);
+    st(a.dv_o + o + b, s + h);
+}
+
 int main(int argc, char **argv)
 {
     const long nodes = argc > 1 ? atol(argv[1]) : 1200000;
     const int L = argc > 2 ? atoi(argv[2]) : 80;
-    const bool json = argc > 3 && std::string(argv[3]) == "--json";
+    const bool json = argc > 3 && std::string(argv[3]) == "--json";  // "--text" (or anything else): a table
     double copy_tbs = 0, cols_tbs = 0;
     const long cn = nodes * L, cnl = nodes * (L + 1);
     std::vector<double *> bufs;
@@ -222,6 +255,35 @@ int main(int argc, char **argv)
         timeit("cols G=8 no XCD swizzle", bytes_p1, [&] {
             hipLaunchKernelGGL(k_cols, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L, G, 0);
         });
+    }
+    // --tracers T (4th argument): the batched pattern at G = 6 and 8 columns, tracer fastest/slowest
+    const int T = argc > 4 ? atoi(argv[4]) : 0;
+    if (T > 1 && L % 2 == 0) {
+        Arrays bt = a;
+        const size_t ts = (size_t)cnl;
+        bt.ttf = alloc(T * cnl);
+        bt.LO = alloc(T * cnl);
+        bt.adfv = alloc(T * cnl);
+        bt.dv = alloc(T * cnl);
+        bt.adfh = alloc(3 * T * cnl);
+        bt.plus = alloc(T * cnl);
+        bt.minus = alloc(T * cnl);
+        bt.adfv_o = const_cast<double *>(bt.adfv);
+        bt.dv_o = const_cast<double *>(bt.dv);
+        const double bytes_b = 8.0 * cn * (4 + T * (4 + 3 + 4));  // shared 4 reads; per tracer 7 reads + 4 writes
+        for (int G : {6, 8})
+            for (int major = 0; major < 2; major++) {
+                char nm[64];
+                snprintf(nm, sizeof nm, "batch T=%d G=%d %s", T, G, major ? "tracer-slowest" : "tracer-fastest");
+                const int thr = ((G * (L / 2) + 63) / 64) * 64;
+                const unsigned groups = (unsigned)((nodes + G - 1) / G);
+                const double r = timeit(nm, bytes_b, [&] {
+                    hipLaunchKernelGGL(k_cols_batch, dim3(groups * T), dim3(thr), 0, 0, bt, (int)nodes, L, G, T, ts, major);
+                });
+                if (json)
+                    printf("{\"batch_GBps\": %.1f, \"tracers\": %d, \"G\": %d, \"order\": \"%s\"}\n", r * 1e3, T, G,
+                           major ? "tracer-slowest" : "tracer-fastest");
+            }
     }
     if (json)
         printf("{\"copy_GBps\": %.1f, \"p1v_pattern_GBps\": %.1f, \"nodes\": %ld, \"levels\": %d}\n", copy_tbs * 1e3,
