@@ -526,8 +526,10 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         flux = m[c] * a.dt * ai[c] - a.eps;
         om[c] = RMIN(1., (tn - lo[c]) / flux);
     }
-    stv_s<C, NT>(a.plus + b, op, nw);
-    stv_s<C, NT>(a.minus + b, om, nw);
+    // OPT & 128 (tuning build): plus/minus as plain stores, so the Infinity Cache may keep them
+    // for b3h's gathers
+    stv_s<C, NT && !(OPT & 128)>(a.plus + b, op, nw);
+    stv_s<C, NT && !(OPT & 128)>(a.minus + b, om, nw);
     }
     if constexpr (VERT) {
         // ---- b3-vertical + c-vertical on the own column (as k_p2: docs/refactoring.md:204-233, :295-300)
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(1024) void k_b3h_g(const int4 *__restrict__ einfo, 
 // REG (reg = {P, s, first edge, edge count}): every edge of the list has s slots, so the greedy
 // packing gave each block P = min(kB3hPackEdges, cap / s) consecutive edges (the last block fewer):
 // a block computes its slice instead of loading a descriptor first, and drops the slot offsets.
-template <bool NT, bool ODD, int H = 2, bool REG = false>
+template <bool NT, bool ODD, int H = 2, bool REG = false, bool STNT = NT>
 __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, const unsigned short *__restrict__ off,
                                                 const int4 *__restrict__ einfo, int L, const real *__restrict__ plus,
                                                 const real *__restrict__ minus, real *__restrict__ adf_h, Tracers trs,
@@ -812,7 +814,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
         real out[C];
 #pragma unroll
         for (int c = 0; c < C; c++) out[c] = b3h_factor(f[h][c], p1[h][c], m1[h][c], p2[h][c], m2[h][c]) * f[h][c];
-        stv_s<C, NT>(adf_h + (size_t)ei.w * L + z0[h], out, nw);
+        stv_s<C, STNT>(adf_h + (size_t)ei.w * L + z0[h], out, nw);  // STNT: tuning (FESOM2_B3H_STPLAIN)
     }
 }
 
@@ -1429,6 +1431,22 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #undef F2A_P1B
         }
     }
+    // FESOM2_PM_PLAIN = 1: the production forms with plus/minus stored as plain (cache-allocating)
+    // stores, the other single-use streams non-temporal as in the product
+    if (knob("FESOM2_PM_PLAIN", 0) && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = plan_columns(S, mp);
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const size_t lds = p1_lds_bytes(G, L, 1, in);
+            const float inv = 1.0f / (float)S;
+            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 128, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 128, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 128>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 128>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+    }
     // FESOM2_P1V_WAVES = W: the production forms held to W waves/SIMD
     if (const int W = knob("FESOM2_P1V_WAVES", 0); W >= 6 && a.vlimit == 1) {
         const int L = a.nl - 1;
@@ -1679,6 +1697,17 @@ static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const
     const bool NT = knob("FESOM2_B3H_NT", 1) != 0;
     int H = knob("FESOM2_B3HP_H", 2);
     if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
+    if (knob("FESOM2_B3H_STPLAIN", 0) && reg.x > 0) {  // the limited fluxes as plain (cache-allocating) stores
+        const dim3 grid((unsigned)groups), block((cap + 1) / 2);
+        if (L % 2)
+            hipLaunchKernelGGL((k_b3h_p<true, true, 2, true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus,
+                               minus, adf_h, tr, reg);
+        else
+            hipLaunchKernelGGL((k_b3h_p<true, false, 2, true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus,
+                               minus, adf_h, tr, reg);
+        *err = hipGetLastError();
+        return true;
+    }
     if (H != 2 || !NT || !knob("FESOM2_B3HP_REG", 1)) {
         const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
         if (H == 1)
