@@ -902,8 +902,12 @@ def extra_legs(args, world):
     strong = ("config4_strong_" + args.strong_config.replace(" ", "").replace(".", "p"),
               dict(config=args.strong_config, tracers=1, scaling="strong"))
     if world == 1:
-        return [("config1_127kx47", dict(config="127k x 47", tracers=1, scaling="weak")),
-                ("config1_127kx47_6tracers", dict(config="127k x 47", tracers=6, scaling="weak")),
+        # the small partition's legs time at least ~0.1 s (a 20-step region of 0.28 ms passes is
+        # 6 ms, where the clocks' ramp after setup still shows)
+        return [("config1_127kx47", dict(config="127k x 47", tracers=1, scaling="weak",
+                                         steps=max(args.steps, 400), warmup=max(args.warmup, 20))),
+                ("config1_127kx47_6tracers", dict(config="127k x 47", tracers=6, scaling="weak",
+                                                  steps=max(args.steps, 80), warmup=max(args.warmup, 10))),
                 ("config3_1p2Mx80_6tracers", dict(config="1.2M x 80", tracers=6, scaling="weak")),
                 strong]
     return [strong]

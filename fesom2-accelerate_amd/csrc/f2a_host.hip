@@ -584,6 +584,14 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }
 
+int pass_order(const Plan &plan, int ntr)
+{
+    const MeshPlanDev &d = plan.dev;
+    const long long flux_bytes = (long long)ntr * d.n_edges * (d.nl - 1) * (long long)sizeof(real);
+    const bool on = plan.cache_order >= 0 ? plan.cache_order == 1 : flux_bytes <= kCacheOrderBytes;
+    return on ? (1 | 4 | 8) : 0;
+}
+
 PlanShape plan_shape(bool batched)
 {
     PlanShape s;
@@ -609,6 +617,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     // plan option FESOM2_NUM_KERNELS: the stepwise path stops phase 1 after that many reference
     // steps (the reference's NUM_KERNELS macro, src/fesom2-accelerate.cu:256; alg_state bisection)
     if (const char *nk = getenv("FESOM2_NUM_KERNELS")) plan->num_kernels = atoi(nk);
+    // plan option FESOM2_CACHE_ORDER (pass_order): 0 off, 1 on, unset automatic
+    if (const char *co = getenv("FESOM2_CACHE_ORDER")) plan->cache_order = atoi(co) ? 1 : 0;
     MeshPlanDev &d = plan->dev;
     d.n_owned = n_owned;
     d.n_total = n_total;

@@ -165,9 +165,21 @@ struct Plan {
     uint64_t serial = 0;  // track_object (fct_adf_h's internal-edge marker refers to a plan)
     long long int_cells = 0;  // edge cells of the block-internal edges p1v limits
     int num_kernels = 10;     // stepwise phase 1 stops after this many reference steps
+    int cache_order = -1;     // plan option FESOM2_CACHE_ORDER: -1 automatic, 0 off, 1 on (pass_order)
     bool has_ring = false;
     int lmax_edges = 0;
 };
+
+// Tracers::order of a direction-split or fused pass of `ntr` tracers on `plan`.  When the pass's
+// fct_adf_h fits the 256 MiB Infinity Cache with room to spare (ntr * edges * (nl-1) * 8 B <=
+// kCacheOrderBytes, e.g. 127k x 47: 143 MB), the kernels alternate directions -- phase 1 walks each
+// XCD's tile range backwards, b3h forwards, the node kernel of phase 2 backwards -- so each kernel
+// starts on the lines its predecessor touched last, and b3h stores the limited fluxes
+// cache-allocating for the node kernel; the next pass's phase 1 starts where this pass's phase 2
+// began, i.e. on the cold end (no gain from repeating a benchmark's inputs).  Larger passes keep
+// every kernel forwards with non-temporal flux stores (measured).
+constexpr long long kCacheOrderBytes = 192ll << 20;
+int pass_order(const Plan &plan, int ntr);
 
 // Processing-order options of a plan.  Single-tracer calls use the defaults (16384-node patches
 // for a numbering with locality, the natural block size); calls with ntracers > 1 get a plan of

@@ -175,6 +175,9 @@ struct MeshPlanDev {
 struct Tracers {
     int n = 1;
     size_t node = 0, lev = 0, edge = 0;
+    // pass order (pass_order, f2a_host.hpp): bit 0 the p1 kernels and bit 2 the p2 node kernels
+    // walk each XCD's tile range backwards, bit 3 b3h stores the limited fluxes cache-allocating
+    int order = 0;
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().

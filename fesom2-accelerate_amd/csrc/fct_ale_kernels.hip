@@ -326,7 +326,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
     int tr = 0;
-    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, c_tile_rev & 1);
+    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, (c_tile_rev | a0.tr.order) & 1);
     const int first = grp * G;
     const int ncol = min(G, a0.n_owned - first);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = (L + C - 1) / C;
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, c_tile_rev & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
     if (tr) {
         a.del_h += tr * a.tr.node;
         a.adf_h += tr * a.tr.edge;
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
         real out[C];
 #pragma unroll
         for (int c = 0; c < C; c++) out[c] = b3h_factor(f[h][c], p1[h][c], m1[h][c], p2[h][c], m2[h][c]) * f[h][c];
-        stv_s<C, STNT>(adf_h + (size_t)ei.w * L + z0[h], out, nw);  // STNT: tuning (FESOM2_B3H_STPLAIN)
+        stv_s<C, STNT>(adf_h + (size_t)ei.w * L + z0[h], out, nw);  // !STNT: cache-allocating (pass_order)
     }
 }
 
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
 {
     extern __shared__ real lds[];  // NodeRec[G]
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, c_tile_rev & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
     if (tr) {
         a.plus += tr * a.tr.node;
         a.minus += tr * a.tr.node;
@@ -1697,17 +1697,6 @@ static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const
     const bool NT = knob("FESOM2_B3H_NT", 1) != 0;
     int H = knob("FESOM2_B3HP_H", 2);
     if ((H != 1 && H != 4) || (L % 2) || !NT || (H == 1 && cap > 1024)) H = 2;
-    if (knob("FESOM2_B3H_STPLAIN", 0) && reg.x > 0) {  // the limited fluxes as plain (cache-allocating) stores
-        const dim3 grid((unsigned)groups), block((cap + 1) / 2);
-        if (L % 2)
-            hipLaunchKernelGGL((k_b3h_p<true, true, 2, true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus,
-                               minus, adf_h, tr, reg);
-        else
-            hipLaunchKernelGGL((k_b3h_p<true, false, 2, true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus,
-                               minus, adf_h, tr, reg);
-        *err = hipGetLastError();
-        return true;
-    }
     if (H != 2 || !NT || !knob("FESOM2_B3HP_REG", 1)) {
         const dim3 grid((unsigned)groups), block((cap + H - 1) / H);
         if (H == 1)
@@ -1725,18 +1714,28 @@ static bool launch_b3h_packed(const int2 *desc, const unsigned short *off, const
     }
 #endif
     const dim3 grid((unsigned)groups), block((cap + 1) / 2);
+    // a pass whose fct_adf_h fits the Infinity Cache (Tracers::order bit 3): the limited fluxes as
+    // plain stores, which c-horizontal then reads from the cache (tuning: FESOM2_B3H_STPLAIN forces it)
+    const bool plain = (tr.order & 8) != 0 || knob("FESOM2_B3H_STPLAIN", 0) != 0;
+#define F2A_B3HP(ODD, REG, PLAIN, R)                                                                                   \
+    hipLaunchKernelGGL((k_b3h_p<true, ODD, 2, REG, !(PLAIN)>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, \
+                       adf_h, tr, R)
     if (reg.x > 0) {
-        if (L % 2)
-            hipLaunchKernelGGL((k_b3h_p<true, true, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
-                               adf_h, tr, reg);
-        else
-            hipLaunchKernelGGL((k_b3h_p<true, false, 2, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus,
-                               adf_h, tr, reg);
+        if (L % 2) {
+            if (plain) F2A_B3HP(true, true, true, reg);
+            else F2A_B3HP(true, true, false, reg);
+        } else {
+            if (plain) F2A_B3HP(false, true, true, reg);
+            else F2A_B3HP(false, true, false, reg);
+        }
     } else if (L % 2) {
-        hipLaunchKernelGGL((k_b3h_p<true, true>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        if (plain) F2A_B3HP(true, false, true, none);
+        else F2A_B3HP(true, false, false, none);
     } else {
-        hipLaunchKernelGGL((k_b3h_p<true, false>), grid, block, 0, s, desc + d0, off, einfo, L, plus, minus, adf_h, tr, none);
+        if (plain) F2A_B3HP(false, false, true, none);
+        else F2A_B3HP(false, false, false, none);
     }
+#undef F2A_B3HP
     *err = hipGetLastError();
     return true;
 }

@@ -256,6 +256,7 @@ void fct_ale_pre_comm_acc_(int *alg_state, void **s, void **fct_ttf_max, void **
         f2a::P1Args a{N, NL, *vlimit, nlev_nod, dptr<real>(bttf), dptr<real>(blo), dptr<real>(badfv),
                       dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
                       *dt, *flux_eps, *bignumber};
+        a.tr.order = f2a::pass_order(*plan, 1);  // kernel directions (Infinity Cache reuse)
         if (kernel_path() == 2) {
             // fast mode: b3-vertical (and the block-internal edges' b3-horizontal) while the block's
             // plus/minus are in LDS; inter_comm / post_comm find the marks and do the rest
@@ -382,6 +383,7 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
                   dptr<real>(badfh), dptr<real>(bainv), dptr<real>(bplus), dptr<real>(bminus),
                   *dt, *flux_eps, *bignumber};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
     if (vertical) {
         a.area = dptr<real>(barea);
         a.hnode = dptr<real>(bh);
@@ -511,19 +513,21 @@ void fct_ale_post_comm_acc_(int *alg_state, void **s, void **fct_plus, void **fc
     if (!g_resident && (!h2d(bplus, false, st, false) || !h2d(bminus, false, st, false))) return;  // reference :364-365
     // fused path: the production edge kernel over the plan's edge list (edge index order here)
     const bool stepwise = kernel_path() == 1;
+    f2a::Tracers tro;
+    tro.order = f2a::pass_order(*plan, 1);  // b3h's flux stores (Infinity Cache reuse by the c-step)
     if (!run("fct_ale_b3_horizontal", st, [&] {
             if (ip) {  // interior edges crossing p1v blocks, then the boundary ones
                 const f2a::MeshPlanDev &de = ip->dev;
                 const hipError_t e = f2a::launch_b3h_ext(de, NL, dptr<real>(bplus), dptr<real>(bminus),
-                                                         dptr<real>(badfh), f2a::Tracers{}, st);
+                                                         dptr<real>(badfh), tro, st);
                 const int eb = de.n_edge_interior;
                 if (e != hipSuccess || eb >= E) return e;
                 return f2a::launch_b3h_fused(de, NL, eb, E - eb, dptr<real>(bplus), dptr<real>(bminus),
-                                             dptr<real>(badfh), f2a::Tracers{}, st);
+                                             dptr<real>(badfh), tro, st);
             }
             if (!stepwise && plan->dev.p_edge_info)
                 return f2a::launch_b3h_fused(plan->dev, NL, 0, E, dptr<real>(bplus), dptr<real>(bminus), dptr<real>(badfh),
-                                             f2a::Tracers{}, st);
+                                             tro, st);
             return f2a::launch_b3h(E, NL, dptr<int>(bnle), dptr<int>(bed), dptr<int>(bet), dptr<real>(bplus),
                                    dptr<real>(bminus), dptr<real>(badfh), st);
         }))
@@ -581,6 +585,7 @@ void fct_ale_c_acc_(int *alg_state, void **s, void **del_ttf_advvert, void **del
         // the fast mode's fct_ale_pre_comm_acc_ did c-vertical already: c-horizontal only
         f2a::P2Args a{NL, d.p2_rec, N, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dptr<real>(barea), nullptr,
                       dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
+        a.tr.order = f2a::pass_order(*plan, 1);  // kernel directions (Infinity Cache reuse)
         if (!run("fct_ale_p2h", st, [&] { return f2a::launch_p2h(d, a, st); })) return;
         mark_internal(bdv, nullptr, st);
     } else if (kernel_path() != 1 && d.p2_rec && (L % 2 == 0 || L >= 3)) {
@@ -658,6 +663,7 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                   dptr<real>(bh), dptr<real>(bhn), dptr<real>(barea), dptr<real>(badfv), dptr<real>(badfh),
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
     // b3-horizontal as its own edge kernel, then the node kernel (the alternatives measured slower:
     // DESIGN.md §3)
     {
@@ -742,6 +748,7 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
     f2a::P2Args a{NL, d.p2_rec, n_first, dptr<real>(bplus), dptr<real>(bminus), nullptr, nullptr, nullptr, nullptr,
                   dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
+    a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
     const f2a::MeshPlanDev &de = ip ? ip->dev : d;  // the edge lists b3h runs on
     const int eb = de.n_edge_interior;               // boundary edges (a halo endpoint): [eb, E)
     if (!run("fct_ale_b3_horizontal", st, [&] {
