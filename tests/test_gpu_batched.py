@@ -247,7 +247,8 @@ def test_split_by_direction_partitioned_overlap(comm, internal, nl, monkeypatch)
 @pytest.mark.parametrize("shape", [{}, {"FESOM2_BATCH_GROUP_SHIFT": "0"},
                                    {"FESOM2_BATCH_GROUP_SHIFT": "-2", "FESOM2_BATCH_PATCH": "64"},
                                    {"FESOM2_BATCH_PATCH": "1"}, {"FESOM2_BATCH_GROUP": "6"},
-                                   {"FESOM2_BATCH_GROUP": "5", "FESOM2_BATCH_PATCH": "300"}],
+                                   {"FESOM2_BATCH_GROUP": "5", "FESOM2_BATCH_PATCH": "300"},
+                                   {"FESOM2_CACHE_ORDER": "1"}],
                          ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()) or "default")
 @pytest.mark.parametrize("name,full", [("8k x 20", False), ("127k x 47", True)])
 @pytest.mark.parametrize("internal", ["0", "1"])
