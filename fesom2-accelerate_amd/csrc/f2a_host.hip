@@ -592,6 +592,62 @@ int pass_order(const Plan &plan, int ntr)
     return on ? (1 | 4 | 8) : 0;
 }
 
+// Row pairs inside an ascending patch (`cur`, first position `base` of the processing order): the
+// patch's runs of consecutive node numbers are its grid rows; each p1v block of G positions takes
+// G/2 consecutive nodes of one row and the G - G/2 nodes right below them in the next row, so the
+// vertical and diagonal edges between the two rows fall inside blocks too (structured 1.2M x 80:
+// 29 % -> 53 % block-internal edges, which p1v limits and b3h then skips).  Two runs pair when both
+// hold at least G nodes and the upper one's first node has a neighbour in the lower one, which
+// aligns the lower row under the upper; the lower row's nodes left of that follow the pair.  A
+// numbering without long rows (space-filling curves, scattered) keeps its ascending order.
+static void row_pairs(std::vector<int> &cur, size_t base, int G, const std::vector<int> &ptr,
+                      const std::vector<int> &other)
+{
+    if (G < 2 || cur.size() < 2) return;
+    std::vector<std::pair<size_t, size_t>> runs;  // [begin, end) in cur
+    size_t s0 = 0;
+    for (size_t i = 1; i <= cur.size(); i++)
+        if (i == cur.size() || cur[i] != cur[i - 1] + 1) {
+            runs.emplace_back(s0, i);
+            s0 = i;
+        }
+    std::vector<int> out;
+    out.reserve(cur.size());
+    const size_t g = (size_t)G, hA = g / 2, hB = g - hA;
+    size_t r = 0;
+    while (r < runs.size()) {
+        const size_t a0 = runs[r].first, a1 = runs[r].second;
+        bool paired = false;
+        if (r + 1 < runs.size() && a1 - a0 >= g && runs[r + 1].second - runs[r + 1].first >= g) {
+            const size_t b0 = runs[r + 1].first, b1 = runs[r + 1].second;
+            // the upper row up to the block grid, then its next node's first neighbour below
+            size_t ka = a0;
+            const size_t align = (g - (base + out.size()) % g) % g;
+            const int v = cur[std::min(a0 + align, a1 - 1)], B0 = cur[b0], nB = (int)(b1 - b0);
+            int first = nB;
+            for (int k = ptr[v]; k < ptr[v + 1]; k++)
+                if (other[k] >= B0 && other[k] < B0 + nB) first = std::min(first, other[k] - B0);
+            if (first < nB && a0 + align < a1) {
+                for (; ka < a0 + align; ka++) out.push_back(cur[ka]);
+                size_t kb = b0 + (size_t)first;
+                const size_t lead = kb;
+                while (ka < a1 || kb < b1) {
+                    for (size_t t = 0; t < hA && ka < a1; t++) out.push_back(cur[ka++]);
+                    for (size_t t = 0; t < hB && kb < b1; t++) out.push_back(cur[kb++]);
+                }
+                out.insert(out.end(), cur.begin() + b0, cur.begin() + lead);
+                paired = true;
+                r += 2;
+            }
+        }
+        if (!paired) {
+            out.insert(out.end(), cur.begin() + a0, cur.begin() + a1);
+            r += 1;
+        }
+    }
+    cur.swap(out);
+}
+
 PlanShape plan_shape(bool batched)
 {
     PlanShape s;
@@ -840,6 +896,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     }
                 } else {
                     std::sort(cur.begin(), cur.end());
+                    if (knob("FESOM2_ROWPAIR", 0))
+                        row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other);
                 }
                 npatch++;
                 order.insert(order.end(), cur.begin(), cur.end());
