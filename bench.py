@@ -125,6 +125,32 @@ def kernel_bytes(s, ntr=1, split=False):
             "pass": p1 + b3h + p2, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 
+def reference_byte_models(m):
+    """The reference's own per-kernel byte models -- what its kernel_tuner scripts divide by the
+    kernel time to print GB/s -- evaluated on this mesh, for the one-kernel-per-step
+    path (--path stepwise): a1 `kernels/fct_ale_a1.py:93`, a2 `fct_ale_a2.py:102-111`, a3
+    `fct_ale_a3.py:116-149`, b1v `fct_ale_b1_vertical.py:149`, b1h `fct_ale_b1_horizontal.py:70-88`,
+    b2 `fct_ale_b2.py:102`, b3v `fct_ale_b3_vertical.py:219`, b3h `fct_ale_b3_horizontal.py:77-100`,
+    cv `fct_ale_c_vertical.py:90`, ch `fct_ale_c_horizontal.py:54-70` (fp64)."""
+    N, H, T = m.N, m.H, m.T
+    ln = m.nlev_nod.astype(np.int64) - 1
+    used_all = int(ln.sum())                 # a1 runs over owned + halo nodes
+    used = int(ln[:N].sum())
+    le = m.nlev_elem.astype(np.int64)
+    wet_e = int(np.maximum(le - 1, 0).sum())
+    fill_e = int(np.maximum(m.nl - 1 - le, 0).sum())
+    nelem = m.nie_num[:N].astype(np.int64)
+    a3 = int((4 + ln[:N] * (20 + 20 * nelem) + 32 * ln[:N]).sum())
+    t = m.edge_tri.reshape(-1, 2)
+    per_edge = int((12 + np.where(t[:, 1] > 0, 8, 4)).sum())
+    ce = m.edge_cells
+    return {"fct_ale_a1": 4 * (N + H) + 32 * used_all, "fct_ale_a2": 16 * T + 64 * wet_e + 16 * fill_e,
+            "fct_ale_a3": a3, "fct_ale_b1_vertical": 4 * N + 32 * used, "fct_ale_b1_horizontal": per_edge + 40 * ce,
+            "fct_ale_b2": 4 * N + 56 * used, "fct_ale_b3_vertical": 4 * N + 24 * N + 48 * used,
+            "fct_ale_b3_horizontal": per_edge + 48 * ce, "fct_ale_c_vertical": 4 * N + 72 * used,
+            "fct_ale_c_horizontal": per_edge + 56 * ce}
+
+
 def kernel_bytes_min(s, ntr=1):
     """SURVEY.md 8(d)'s strict minimum bytes for the work of the phase-1 kernels (each array of its
     table read or written once, no index arrays, no halo columns, no internal-edge flux writes):
@@ -781,6 +807,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     kb = kernel_bytes(s, args.tracers, split=args.path in ("split", "reference"))
     kbm = kernel_bytes_min(s, args.tracers)
     per_kernel = {}
+    refm = reference_byte_models(m) if args.path == "stepwise" and args.tracers == 1 else None
     for name, (cnt, tot) in list(stats.items()) + [kv for kv in breakdown.items() if kv[0] not in stats]:
         a_ms = tot / max(cnt, 1)
         entry = {"launches": cnt, "avg_ms": round(a_ms, 4),
@@ -788,6 +815,9 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         if name in kb:
             entry["alg_bytes"] = kb[name]
             entry["GBps"] = round(kb[name] / (a_ms * 1e-3) / 1e9, 1)
+        if refm and name in refm:  # the reference harness's own bandwidth figure for this kernel
+            entry["ref_model_bytes"] = refm[name]
+            entry["ref_model_GBps"] = round(refm[name] / (a_ms * 1e-3) / 1e9, 1)
         per_kernel[name] = entry
     dom = max(stats, key=lambda k: stats[k][1]) if stats else None
     traffic = None

@@ -234,3 +234,43 @@ def test_watchdog_exits_with_the_stage_on_stderr():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert out.returncode == 3
     assert "rank 5: watchdog: stage 'RCCL communicator setup' not done within 1 s" in out.stderr
+
+
+def test_reference_byte_models_follow_the_scripts_loops():
+    """reference_byte_models evaluates the reference's kernel_tuner byte counters in closed form;
+    here they are recounted with the scripts' own loops (kernels/fct_ale_a3.py:116-149,
+    fct_ale_b1_horizontal.py:70-88, fct_ale_a2.py:102-111) on a small mesh with variable depth."""
+    m = synth.config_mesh("tiny", full_depth=False)
+    got = bench.reference_byte_models(m)
+    levels = m.nlev_nod.astype(int)
+    nelem = m.nie_num.astype(int)
+    a3 = 0
+    for node in range(m.N):
+        a3 += 4
+        for _ in range(levels[node] - 1):
+            a3 += 4 + 16 + nelem[node] * (4 + 16)
+        a3 += 4 * 8 + max(0, levels[node] - 3) * 4 * 8 + 4 * 8
+    assert got["fct_ale_a3"] == a3
+    b1h = 0
+    t = m.edge_tri.reshape(-1, 2)
+    le = m.nlev_elem.astype(int)
+    for e in range(m.E):
+        b1h += 12
+        one = t[e, 0] - 1
+        if t[e, 1] <= 0:
+            b1h += 4
+            n = max(le[one] - 1, 0)
+        else:
+            b1h += 8
+            n = max(le[one] - 1, le[t[e, 1] - 1] - 1)
+        b1h += n * 5 * 8
+    assert got["fct_ale_b1_horizontal"] == b1h
+    a2 = 16 * m.T
+    for el in range(m.T):
+        a2 += max(le[el] - 1, 0) * 8 * 8
+        if le[el] <= m.nl - 1:
+            a2 += (m.nl - 1 - le[el]) * 2 * 8
+    assert got["fct_ale_a2"] == a2
+    used = int((levels[: m.N] - 1).sum())
+    assert got["fct_ale_b2"] == 4 * m.N + 7 * 8 * used
+    assert got["fct_ale_c_vertical"] == 4 * m.N + 9 * 8 * used
