@@ -633,6 +633,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     dm.prepare()
     mi = dm.info(batched=args.tracers > 1)
     mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
+    order = dm.pass_order(args.tracers)  # the Infinity-Cache pass order the entries use
     if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or args.transfers):
         raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
     e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
@@ -893,7 +894,8 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
                              "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
                              "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
            "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
-           "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s}
+           "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s,
+           "pass_order": order}
     if world > 1:
         ms = [r[0] for r in per_rank]
         rec["ranks"] = {
@@ -952,7 +954,7 @@ def compact(rec, args, world):
            "nodes_per_gpu": m.N, "levels": m.L, "cells_per_gpu": s["cn"], "tracers": args.tracers,
            "roofline": rec["roofline"], "pass_roofline": rec["pass_roofline"],
            "kernels_ms": {k: v["avg_ms"] for k, v in rec["kernels"].items()}, "check": rec["check"],
-           "setup_s": rec["setup_s"]}
+           "setup_s": rec["setup_s"], "pass_order": rec["pass_order"]}
     for k in ("ranks", "rccl_nranks"):
         if k in rec:
             out[k] = rec[k]
@@ -1104,6 +1106,7 @@ def main():
         "transfers": "reference transfer semantics, PCIe inside the timed step" if args.transfers else
                      "device resident (inputs in HBM before the timed region)",
         "setup_s": head["setup_s"],
+        "pass_order": head["pass_order"],
     }
     if head["check"] is not None:
         out["check"] = head["check"]

@@ -976,6 +976,32 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
 // endpoints owned), [2] interior edges crossing p1v blocks (b3h's), [3] block-internal edges
 // (limited inside p1v), [4] their edge cells (sum of levels); [5, 10) the same for the plan of batched
 // calls (ntracers > 1, built here if needed).  *ninfo: entries wanted (<= 10) / written.
+// The Infinity-Cache pass order (f2a::pass_order) the split, fused and reference-sequence entries
+// use for a call of `ntracers` tracers on this mesh (plan built if needed).
+void fesom2_pass_order_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                        void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                        int *ntracers, int *order)
+{
+    *istat = 1;
+    *order = 0;
+    const int N = *myDim_nod2D, NT = N + *eDim_nod2D, E = *myDim_edge2D, NL = *nl, ntr = *ntracers;
+    if (!check_levels(NL, "fesom2_pass_order_")) return;
+    if (ntr < 1) {
+        report("fesom2_pass_order_: ntracers = %d", ntr);
+        return;
+    }
+    MeshHandles mh;
+    mh.edges = need(nod2D_edges, 2 * sizeof(int) * (size_t)E, "nod2D_edges");
+    mh.edge_tri = need(elem2D_edges, 2 * sizeof(int) * (size_t)E, "elem2D_edges");
+    mh.nlev_elem = buf(nlevels_elem2D, "nlevels_elem2D");
+    mh.nlev_nod = need(nlevels_nod2D, sizeof(int) * (size_t)N, "nlevels_nod2D");
+    if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !mh.nlev_nod) return;
+    const Plan *plan = get_plan(mh, N, NT, E, NL, false, ntr > 1);
+    if (!plan) return;
+    *order = f2a::pass_order(*plan, ntr);
+    *istat = 0;
+}
+
 void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
                        int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
                        void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,

@@ -32,7 +32,7 @@ EXPORTS = (
     "fct_ale_post_comm_iter_batched_acc_", "fesom2_exchange_nod_acc_",
     "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_", "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_",
     "fesom2_graph_begin_", "fesom2_graph_end_", "fesom2_graph_launch_", "fesom2_graph_free_",
-    "fesom2_graph_info_", "fesom2_mesh_info_", "fesom2_bind_c_vertical_",
+    "fesom2_graph_info_", "fesom2_mesh_info_", "fesom2_bind_c_vertical_", "fesom2_pass_order_",
 )
 
 # the reference's C++ convenience entries (include/fesom2-accelerate-legacy.hpp: C linkage, plain

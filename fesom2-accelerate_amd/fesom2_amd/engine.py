@@ -68,6 +68,18 @@ class DeviceMesh:
         vals = list(out)[: n.value]
         return dict(zip(keys, vals[5:] if batched else vals))
 
+    def pass_order(self, ntracers=1):
+        """fesom2_pass_order_: the Infinity-Cache pass order of a call of ``ntracers`` tracers
+        (bits 1 / 4: phase 1 / the c-step's node kernel backwards, 8: b3h's flux stores
+        cache-allocating; 0: off)."""
+        m, h = self.m, self.h
+        st, order = C.c_int(0), C.c_int(0)
+        dll().fesom2_pass_order_(C.byref(st), ip(m.N), ip(m.H), ip(m.E), ip(m.nl), h["nlev_nod"].ref,
+                                 h["nlev_elem"].ref, h["edges"].ref, h["edge_tri"].ref, ip(ntracers),
+                                 C.byref(order))
+        check(st, "fesom2_pass_order_")
+        return order.value
+
     def free(self):
         for h in self.h.values():
             if h:

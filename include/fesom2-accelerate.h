@@ -161,6 +161,15 @@ void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim
                        int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
                        void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,
                        void **nod2D_edges, void **elem2D_edges, long long *info, int *ninfo);
+/* The Infinity-Cache pass order the split, fused and reference-sequence entries use for a call of
+ * *ntracers tracers on this mesh (mesh plan built if needed): *order bits 1 phase 1 and 4 the
+ * c-step's node kernel walk their tile ranges backwards, 8 b3h stores the limited fluxes
+ * cache-allocating; 0 = every kernel forwards with non-temporal flux stores.  On when the call's
+ * fct_adf_h (ntracers x myDim_edge2D x (nl-1) doubles) is at most 192 MiB, or as the plan option
+ * FESOM2_CACHE_ORDER forces.  Results never depend on it. */
+void fesom2_pass_order_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_edge2D, int *nl,
+                        void **nlevels_nod2D, void **nlevels_elem2D, void **nod2D_edges, void **elem2D_edges,
+                        int *ntracers, int *order);
 /* Copy a handle's device contents to/from a host array (no rebinding), synchronous. */
 void fesom2_download_(void **mem, void *host_ptr, int *istat);
 void fesom2_upload_(void **mem, void *host_ptr, int *istat);

@@ -302,3 +302,27 @@ def test_batched_plan_of_a_large_partition():
     finally:
         dm.free()
 
+
+
+@pytest.mark.parametrize("env,expect", [(None, {1: 13, 2: 0, 6: 0}), ("0", {1: 0, 2: 0, 6: 0}),
+                                        ("1", {1: 13, 2: 13, 6: 13})])
+def test_pass_order_rule(env, expect, monkeypatch):
+    """fesom2_pass_order_ reports the Infinity-Cache pass order the entries use: on 127k x 47 (one
+    tracer's fct_adf_h 143 MB <= 192 MiB) for one tracer, off for two (286 MB) and six; the plan
+    option FESOM2_CACHE_ORDER forces it either way.  8k x 20 keeps it for six tracers (23 MB)."""
+    if env is not None:
+        monkeypatch.setenv("FESOM2_CACHE_ORDER", env)
+    else:
+        monkeypatch.delenv("FESOM2_CACHE_ORDER", raising=False)
+    m = synth.config_mesh("127k x 47", full_depth=True)
+    dm = engine.DeviceMesh(m)
+    try:
+        assert {t: dm.pass_order(t) for t in expect} == expect
+    finally:
+        dm.free()
+    if env is None:
+        small = engine.DeviceMesh(synth.config_mesh("8k x 20"))
+        try:
+            assert small.pass_order(6) == 13
+        finally:
+            small.free()
