@@ -357,7 +357,7 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
 template <int C, int kBatch, bool ODD = false, class F>
 __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int e0, int e1,
                                           const real *__restrict__ adf_h, int z0, int L, F &&f,
-                                          bool last1 = false)
+                                          bool last1 = false, real *stash = nullptr)
 {
     const int zl = z0;  // odd L: the last pair reads one level past the column (ldo)
     for (int k0 = e0; k0 < e1; k0 += kBatch) {
@@ -372,18 +372,28 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
         real h[kBatch][C];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            if (z0 < (code[k] >> 1)) {
+            if (z0 < ((code[k] >> 1) & kLevMask)) {
                 ldo_pre<C, ODD>(adf_h + idx[k], h[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;
             }
         }
+        if (stash) {  // tuning (FESOM2_P1V_STASH): the block-internal edges' raw flux into LDS
+#pragma unroll
+            for (int k = 0; k < kBatch; k++) {
+                const int sl = code[k] >> kStashShift;
+                if (sl)
+#pragma unroll
+                    for (int c = 0; c < C; c++)
+                        if (z0 + c < ((code[k] >> 1) & kLevMask)) stash[(sl - 1) * L + z0 + c] = h[k][c];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kBatch; k++)
 #pragma unroll
             for (int c = 0; c < C; c++)
-                if (z0 + c < (code[k] >> 1)) f(c, h[k][c], code[k] & 1);
+                if (z0 + c < ((code[k] >> 1) & kLevMask)) f(c, h[k][c], code[k] & 1);
     }
 }
 
@@ -404,7 +414,7 @@ __device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ ed
         real h[kBatch][C], po[kBatch][C], mo[kBatch][C];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            if (z0 < (er[k].code >> 1)) {
+            if (z0 < ((er[k].code >> 1) & kLevMask)) {
                 ldo<C, ODD>(adf_h + (size_t)er[k].edge * L + z0, h[k], last1);
                 ldo<C, ODD>(plus + (size_t)er[k].other * L + z0, po[k], last1);
                 ldo<C, ODD>(minus + (size_t)er[k].other * L + z0, mo[k], last1);
@@ -412,7 +422,7 @@ __device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ ed
         }
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            const int lev = er[k].code >> 1, second = er[k].code & 1;
+            const int lev = (er[k].code >> 1) & kLevMask, second = er[k].code & 1;
 #pragma unroll
             for (int c = 0; c < C; c++) {
                 if (z0 + c >= lev) continue;

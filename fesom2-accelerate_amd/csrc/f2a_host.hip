@@ -688,6 +688,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     long long wet_cells = 0;  // owned wet cells (the size rules below and FESOM2_P1V_B3H)
     if (m.nlev_nod)
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
+    // a batch on a large partition: smaller blocks (below), row-pair blocks and the internal edges'
+    // raw flux kept in LDS (row_pairs, MeshPlanDev::int_stash; tuning: FESOM2_ROWPAIR, FESOM2_P1V_STASH)
+    bool batch_large = false;
     if (d.gshift == PlanShape::kAuto) {
         // a batch on a large partition (>= 32M owned wet cells): smaller blocks -- the largest column
         // count below the natural one that keeps >= 90 % of the block's lanes busy.  Measured, 6
@@ -697,6 +700,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // (5 columns: +1.6 %, 7: +0.6 %), so small partitions keep the single plan's shape.
         d.gshift = 0;
         if (wet_cells >= (32ll << 20)) {
+            batch_large = true;
             const int S = p1v_slots(nl), Gn = p1v_group_columns(nl, 0);
             for (int g = Gn - 1; g >= 1; g--)
                 if (10 * g * S >= 9 * ((g * S + 63) / 64 * 64) && g * (nl - 1) <= 1024) {
@@ -896,7 +900,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     }
                 } else {
                     std::sort(cur.begin(), cur.end());
-                    if (knob("FESOM2_ROWPAIR", 0))
+                    // row pairs: batched calls on large partitions (6 x 1.2M x 80 with the stash below:
+                    // -1.8 %); the single-tracer plan measured neutral (not adopted)
+                    if (knob("FESOM2_ROWPAIR", batch_large ? 1 : 0))
                         row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other);
                 }
                 npatch++;
@@ -989,7 +995,22 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 if (!pack_edges(ext, {0, (int)ext.size()}, xcap, xdesc, xoff, xends))
                     return fail("packing the crossing edges failed");
                 d.int_G = IG;
+                d.int_max = most;
                 for (const int4 &ie : iedges) plan->int_cells += ie.w;
+                // the LDS stash (batched calls on large partitions; tuning: FESOM2_P1V_STASH): mark each
+                // internal edge's first-endpoint EdgeRef with its slot in the block's list, for the
+                // NodeRecs and p_edges built below
+                if (knob("FESOM2_P1V_STASH", batch_large ? 1 : 0) && L <= kLevMask) {
+                    for (int b = 0; b < nblk; b++)
+                        for (int k = iptr[b]; k < iptr[b + 1]; k++) {
+                            const int4 ie = iedges[k];  // {edge, column of edges(1,e), column of edges(2,e), lev}
+                            const NodeInfo &n1 = info[b * IG + ie.y];
+                            for (int q = n1.e0; q < n1.e1; q++)
+                                if (pedges[q].edge == ie.x && !(pedges[q].code & 1))
+                                    pedges[q].code |= (k - iptr[b] + 1) << kStashShift;
+                        }
+                    d.int_stash = 1;
+                }
                 d.int_ptr = plan->mem.upload(iptr);
                 d.int_edges = plan->mem.upload(iedges);
                 d.n_ext_interior = (int)ext.size();

@@ -158,6 +158,11 @@ struct MeshPlanDev {
     // block's LDS after b2): for p1v block b (int_G positions of the processing order) the entries
     // int_edges[int_ptr[b] .. int_ptr[b+1]) = {edge, column of edges(1,e), column of edges(2,e), lev}
     int int_G = 0;                        // 0: no internal-edge lists
+    int int_max = 0;                      // most internal edges of one block
+    // tuning build (FESOM2_P1V_STASH): the first endpoint's EdgeRef of each internal edge carries
+    // (slot + 1) << kStashShift, slot = the edge's index in its block's list; p1v then keeps the
+    // raw flux its b1h gather read in an LDS stash instead of re-reading it for the limiter
+    int int_stash = 0;
     const int *int_ptr = nullptr;
     const int4 *int_edges = nullptr;
     // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
@@ -206,6 +211,8 @@ int p1v_slots(int nl);
 // launch_p1v limits the block-internal edges' fct_adf_h itself (b3h must then skip them)
 bool p1v_limits_internal(const MeshPlanDev &mp, const P1Args &a);
 constexpr int kMaxInternal = 64;  // most block-internal edges a p1v block limits (LDS staging)
+constexpr int kStashShift = 12;   // EdgeRef::code bits above the level count (lev < 2048) and `second`
+constexpr int kLevMask = 0x7FF;
 // LDS of that staging (int4 entries + int slot offsets), rounded to whole doubles
 __host__ __device__ constexpr size_t p1_internal_lds_bytes()
 {

@@ -365,6 +365,11 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     // (behind the records and the internal-edge staging: p1_lds_bytes)
     real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
+    // OPT & 256 (tuning, FESOM2_P1V_STASH, with OPT & 16): the internal edges' raw flux, kept by
+    // the first endpoint's b1h gather ([slot][level], behind every other region)
+    real *stash = nullptr;
+    if constexpr (VERT && (OPT & 16) && (OPT & 256))
+        stash = cmx + (VLIMIT != 1 ? G * L : 0);
     const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
         if (t < int_n)  // wave 0 (int_n <= kMaxInternal = kWave): lane t's entry lands at ie_ent[t]
@@ -452,8 +457,9 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 m[c] += RMIN(0., h);
             }
         };
-        for_edges<C, EB, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1);
-        if (ne > kRecEdge) for_edges<C, EB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1);
+        for_edges<C, EB, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1, stash);
+        if (ne > kRecEdge)
+            for_edges<C, EB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1, stash);
     }
     real *tvx = lds, *tvn = lds + G * L;
     const int q = j * L + z0;
@@ -569,9 +575,14 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
                 const int zi = C * (w - ie_off[lo_k]);
                 const bool l1 = ODD && zi + 1 == L;
                 real f[C], out[C];
-                ldo<C, ODD>(a.adf_h + (size_t)e.x * L + zi, f, l1);
-                const int q1 = e.y * L + zi, q2 = e.z * L + zi;
                 const int nwi = min(C, e.w - zi);
+                if constexpr ((OPT & 256) != 0) {
+#pragma unroll
+                    for (int c = 0; c < C; c++) f[c] = c < nwi ? stash[lo_k * L + zi + c] : 0.;
+                } else {
+                    ldo<C, ODD>(a.adf_h + (size_t)e.x * L + zi, f, l1);
+                }
+                const int q1 = e.y * L + zi, q2 = e.z * L + zi;
 #pragma unroll
                 for (int c = 0; c < C; c++)
                     out[c] = c < nwi ? b3h_factor(f[c], pl[q1 + c], mn[q1 + c], pl[q2 + c], mn[q2 + c]) * f[c] : 0.;
@@ -1431,6 +1442,24 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #undef F2A_P1B
         }
     }
+    // FESOM2_P1V_STASH = 1 (plan built with the stash marks): the internal-edge forms keep the
+    // internal edges' raw flux from b1h in LDS (int_max x L doubles more) instead of re-reading it
+    if (mp.int_stash && in && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = plan_columns(S, mp);
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const size_t lds = p1_lds_bytes(G, L, 1, in) + (size_t)mp.int_max * L * sizeof(real);
+            const float inv = 1.0f / (float)S;
+            if (knob("FESOM2_P1V_STASH", 1) == 2) {  // held to 8 waves/SIMD
+                if (odd) F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 256, true>), groups, G, S, lds, s, mp, a, G, inv);
+                F2A_LAUNCH_GROUPS((k_p1o<8, 1, 2, 2, 2, true, true, 52 | 256>), groups, G, S, lds, s, mp, a, G, inv);
+            }
+            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+    }
     // FESOM2_PM_PLAIN = 1: the production forms with plus/minus stored as plain (cache-allocating)
     // stores, the other single-use streams non-temporal as in the product
     if (knob("FESOM2_PM_PLAIN", 0) && a.vlimit == 1) {
@@ -1473,8 +1502,17 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #else
     const int L = a.nl - 1;
     // OPT 4: 16-byte loads/stores of the stride-nl arrays; +16 the block-internal edges'
-    // b3-horizontal, +32 their entries staged into LDS by DMA.  NT: the single-use streams
-    // (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
+    // b3-horizontal, +32 their entries staged into LDS by DMA, +256 their raw flux kept in LDS by
+    // the b1h gather (plans with MeshPlanDev::int_stash: batched calls on large partitions).  NT: the
+    // single-use streams (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
+    if (mp.int_stash && in && a.vlimit == 1 && (odd_pairs(L) || levels_per_thread(L) == 2)) {
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
+        const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+        const size_t lds = p1_lds_bytes(G, L, 1, in) + (size_t)mp.int_max * L * sizeof(real);
+        const float inv = 1.0f / (float)S;
+        if (odd_pairs(L)) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256, true>), groups, G, S, lds, s, mp, a, G, inv);
+        F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256>), groups, G, S, lds, s, mp, a, G, inv);
+    }
     if (odd_pairs(L)) {  // odd L in level pairs, every vlimit (the 3-point bounds of vlimit 2/3 skip the pad level)
         const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;

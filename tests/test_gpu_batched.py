@@ -297,8 +297,13 @@ def test_batched_plan_of_a_large_partition():
     m = synth.config_mesh("1.2M x 80", full_depth=True)
     dm = engine.DeviceMesh(m)
     try:
-        assert dm.info()["p1v_columns"] == 8
-        assert dm.info(batched=True)["p1v_columns"] == 6
+        one, many = dm.info(), dm.info(batched=True)
+        assert one["p1v_columns"] == 8
+        assert many["p1v_columns"] == 6
+        # row-pair blocks (3 nodes of a patch row over the 3 below them) in the batched plan: about
+        # half the interior edges are block-internal, against 29 % in the single-tracer plan's rows
+        assert 0.27 < one["internal_edges"] / one["interior_edges"] < 0.31
+        assert many["internal_edges"] / many["interior_edges"] > 0.45
     finally:
         dm.free()
 

@@ -71,7 +71,10 @@ SPLIT_KNOBS = [{"FESOM2_ODD_PAIR": "0"}, {"FESOM2_NL_PAIR": "0"}, {"FESOM2_NL_PA
                {"FESOM2_PM_PLAIN": "1"}, {"FESOM2_PM_PLAIN": "1", "FESOM2_P1V_B3H": "1", "FESOM2_TILE_REV": "2"},
                {"FESOM2_B3H_STPLAIN": "1"}, {"FESOM2_B3H_STPLAIN": "1", "FESOM2_PM_PLAIN": "1", "FESOM2_P1V_B3H": "1", "FESOM2_TILE_REV": "5"},
                {"FESOM2_ROWPAIR": "1"}, {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1"},
-               {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"}]
+               {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"},
+               {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_STASH": "2", "FESOM2_P1V_B3H": "1"},
+               {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1", "FESOM2_ROWPAIR": "1"},
+               {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"}]
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
