@@ -98,6 +98,27 @@ def test_config3_batched_split_pass(name, ntr):
         check_owned(m, {n: got[n][k] for n in FIELDS}, want, f"{name} tracer {k}")
 
 
+def test_fused_batched_entries_on_the_large_batched_plan():
+    """The batched plan of a large partition marks the internal edges' first-endpoint EdgeRefs for
+    p1v's LDS stash (DESIGN.md 3, row pairs + stash); the fused batched entries
+    (fct_ale_pre_comm_batched_acc_ -> fct_ale_post_comm_c_batched_acc_) gather over the same
+    records and must read past the marks: 2 tracers at 1.2M x 80, exact per tracer."""
+    m = synth.config_mesh("1.2M x 80", full_depth=True)
+    tracers = synth.make_tracer_fields(m, 2)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.full_pass(fused=True) == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k).reshape(2, -1) for k in FIELDS}
+    finally:
+        e.free()
+        dm.free()
+    wants = pmap(lambda t: O.full_pass(m, t), tracers)
+    for k, want in enumerate(wants):
+        check_owned(m, {n: got[n][k] for n in FIELDS}, want, f"fused batch tracer {k}")
+
+
 def partitioned_split_pass(locs, fields):
     """Every strip's pre_comm_v on the GPU, the caller's exchange of fct_plus/fct_minus between the
     strips (FESOM's exchange_nod, here by the halo lists through host memory), every strip's
