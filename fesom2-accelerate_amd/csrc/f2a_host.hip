@@ -1000,7 +1000,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 // the LDS stash (batched calls on large partitions; tuning: FESOM2_P1V_STASH): mark each
                 // internal edge's first-endpoint EdgeRef with its slot in the block's list, for the
                 // NodeRecs and p_edges built below
-                if (knob("FESOM2_P1V_STASH", batch_large ? 1 : 0) && L <= kLevMask) {
+                // (the slab is int_max x L doubles of LDS per block: kept to 16 KB, 6.4 KB at 1.2M x 80)
+                if (knob("FESOM2_P1V_STASH", batch_large ? 1 : 0) && L <= kLevMask &&
+                    (size_t)most * L * sizeof(real) <= 16384) {
                     for (int b = 0; b < nblk; b++)
                         for (int k = iptr[b]; k < iptr[b + 1]; k++) {
                             const int4 ie = iedges[k];  // {edge, column of edges(1,e), column of edges(2,e), lev}
