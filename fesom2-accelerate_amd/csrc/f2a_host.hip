@@ -660,7 +660,8 @@ PlanShape plan_shape(bool batched)
         s.gshift = gs ? atoi(gs) : PlanShape::kAuto;
         s.gcols = gc ? std::max(0, atoi(gc)) : 0;
     } else {
-        s.gshift = knob("FESOM2_GROUP_SHIFT", 0);  // tuning build A/B
+        // automatic (the large-partition rule of build_plan) unless the tuning build sets a shape
+        s.gshift = knob("FESOM2_GROUP_SHIFT", PlanShape::kAuto);
         s.gcols = knob("FESOM2_GROUP", 0);
     }
     return s;
@@ -688,19 +689,21 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     long long wet_cells = 0;  // owned wet cells (the size rules below and FESOM2_P1V_B3H)
     if (m.nlev_nod)
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
-    // a batch on a large partition: smaller blocks (below), row-pair blocks and the internal edges'
-    // raw flux kept in LDS (row_pairs, MeshPlanDev::int_stash; tuning: FESOM2_ROWPAIR, FESOM2_P1V_STASH)
-    bool batch_large = false;
+    // a large partition: smaller blocks (below), row-pair blocks and the internal edges' raw flux
+    // kept in LDS (row_pairs, MeshPlanDev::int_stash; tuning: FESOM2_ROWPAIR, FESOM2_P1V_STASH)
+    bool large_auto = false;
     if (d.gshift == PlanShape::kAuto) {
-        // a batch on a large partition (>= 32M owned wet cells): smaller blocks -- the largest column
-        // count below the natural one that keeps >= 90 % of the block's lanes busy.  Measured, 6
-        // tracers at 1.2M x 80 (40 slots; 8 columns natural), one box, 3 interleaved rounds:
-        // 6 columns (240 of 256 lanes) 21.26 ms, 3: 21.52-21.67, 12: 21.65, 4: 21.76, 7: 23.15,
-        // 8 (the single plan): 23.0-23.3.  On 127k x 47 (6M cells) every smaller block loses
-        // (5 columns: +1.6 %, 7: +0.6 %), so small partitions keep the single plan's shape.
+        // a large partition (>= 32M owned wet cells): smaller blocks -- the largest column count below
+        // the natural one that keeps >= 90 % of the block's lanes busy -- taken in row pairs with
+        // the stash (below).  Measured, 6 tracers at 1.2M x 80 (40 slots; 8 columns natural), one
+        // box, 3 interleaved rounds: 6 columns (240 of 256 lanes) 21.26 ms, 3: 21.52-21.67, 12:
+        // 21.65, 4: 21.76, 7: 23.15, 8: 23.0-23.3; with row pairs + stash 6 columns 21.24, 4: 22.05,
+        // 8: 22.43.  One tracer: 6 columns in row pairs with the stash 4.06 ms against 4.14-4.17
+        // with 8 in single rows (-2.2 %), 6 columns alone -0.4 %.  On 127k x 47 (6M cells) every
+        // smaller block loses (5 columns: +1.6 %, 7: +0.6 %): small partitions keep the natural one.
         d.gshift = 0;
         if (wet_cells >= (32ll << 20)) {
-            batch_large = true;
+            large_auto = true;
             const int S = p1v_slots(nl), Gn = p1v_group_columns(nl, 0);
             for (int g = Gn - 1; g >= 1; g--)
                 if (10 * g * S >= 9 * ((g * S + 63) / 64 * 64) && g * (nl - 1) <= 1024) {
@@ -900,9 +903,9 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     }
                 } else {
                     std::sort(cur.begin(), cur.end());
-                    // row pairs: batched calls on large partitions (6 x 1.2M x 80 with the stash below:
-                    // -1.8 %); the single-tracer plan measured neutral (not adopted)
-                    if (knob("FESOM2_ROWPAIR", batch_large ? 1 : 0))
+                    // row pairs on large partitions, with the stash below (1.2M x 80: -2.2 % with 6
+                    // columns, 6 tracers -1.2 %)
+                    if (knob("FESOM2_ROWPAIR", large_auto ? 1 : 0))
                         row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other);
                 }
                 npatch++;
@@ -997,11 +1000,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                 d.int_G = IG;
                 d.int_max = most;
                 for (const int4 &ie : iedges) plan->int_cells += ie.w;
-                // the LDS stash (batched calls on large partitions; tuning: FESOM2_P1V_STASH): mark each
+                // the LDS stash (large partitions; tuning: FESOM2_P1V_STASH): mark each
                 // internal edge's first-endpoint EdgeRef with its slot in the block's list, for the
                 // NodeRecs and p_edges built below
                 // (the slab is int_max x L doubles of LDS per block: kept to 16 KB, 6.4 KB at 1.2M x 80)
-                if (knob("FESOM2_P1V_STASH", batch_large ? 1 : 0) && L <= kLevMask &&
+                if (knob("FESOM2_P1V_STASH", large_auto ? 1 : 0) && L <= kLevMask &&
                     (size_t)most * L * sizeof(real) <= 16384) {
                     for (int b = 0; b < nblk; b++)
                         for (int k = iptr[b]; k < iptr[b + 1]; k++) {
