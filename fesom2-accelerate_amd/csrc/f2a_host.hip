@@ -592,7 +592,8 @@ int pass_order(const Plan &plan, int ntr)
     return on ? (1 | 4 | 8) : 0;
 }
 
-// Row pairs inside an ascending patch (`cur`, first position `base` of the processing order): the
+// Row pairs (R = 2; the tuning build tries R rows) inside an ascending patch (`cur`, first position
+// `base` of the processing order): the
 // patch's runs of consecutive node numbers are its grid rows; each p1v block of G positions takes
 // G/2 consecutive nodes of one row and the G - G/2 nodes right below them in the next row, so the
 // vertical and diagonal edges between the two rows fall inside blocks too (structured 1.2M x 80:
@@ -601,9 +602,9 @@ int pass_order(const Plan &plan, int ntr)
 // aligns the lower row under the upper; the lower row's nodes left of that follow the pair.  A
 // numbering without long rows (space-filling curves, scattered) keeps its ascending order.
 static void row_pairs(std::vector<int> &cur, size_t base, int G, const std::vector<int> &ptr,
-                      const std::vector<int> &other)
+                      const std::vector<int> &other, int R = 2)
 {
-    if (G < 2 || cur.size() < 2) return;
+    if (G < R || R < 2 || cur.size() < 2) return;
     std::vector<std::pair<size_t, size_t>> runs;  // [begin, end) in cur
     size_t s0 = 0;
     for (size_t i = 1; i <= cur.size(); i++)
@@ -613,34 +614,47 @@ static void row_pairs(std::vector<int> &cur, size_t base, int G, const std::vect
         }
     std::vector<int> out;
     out.reserve(cur.size());
-    const size_t g = (size_t)G, hA = g / 2, hB = g - hA;
+    const size_t g = (size_t)G;
+    std::vector<size_t> take(R), k(R), lead(R);  // nodes per block from each row; cursors; lead ends
+    for (int q = 0; q < R; q++) take[q] = g / R + ((size_t)q >= R - g % R ? 1 : 0);  // the odd ones below
     size_t r = 0;
     while (r < runs.size()) {
         const size_t a0 = runs[r].first, a1 = runs[r].second;
-        bool paired = false;
-        if (r + 1 < runs.size() && a1 - a0 >= g && runs[r + 1].second - runs[r + 1].first >= g) {
-            const size_t b0 = runs[r + 1].first, b1 = runs[r + 1].second;
-            // the upper row up to the block grid, then its next node's first neighbour below
-            size_t ka = a0;
-            const size_t align = (g - (base + out.size()) % g) % g;
-            const int v = cur[std::min(a0 + align, a1 - 1)], B0 = cur[b0], nB = (int)(b1 - b0);
-            int first = nB;
-            for (int k = ptr[v]; k < ptr[v + 1]; k++)
-                if (other[k] >= B0 && other[k] < B0 + nB) first = std::min(first, other[k] - B0);
-            if (first < nB && a0 + align < a1) {
-                for (; ka < a0 + align; ka++) out.push_back(cur[ka]);
-                size_t kb = b0 + (size_t)first;
-                const size_t lead = kb;
-                while (ka < a1 || kb < b1) {
-                    for (size_t t = 0; t < hA && ka < a1; t++) out.push_back(cur[ka++]);
-                    for (size_t t = 0; t < hB && kb < b1; t++) out.push_back(cur[kb++]);
+        bool grouped = false;
+        bool long_rows = r + R <= runs.size();
+        for (int q = 0; long_rows && q < R; q++) long_rows = runs[r + q].second - runs[r + q].first >= g;
+        const size_t align = (g - (base + out.size()) % g) % g;  // the upper row up to the block grid
+        if (long_rows && a0 + align < a1) {
+            // each lower row aligned under the one above: the first neighbour, in the lower row, of
+            // the upper row's first grouped node
+            k[0] = a0 + align;
+            bool ok = true;
+            for (int q = 1; q < R && ok; q++) {
+                const size_t b0 = runs[r + q].first, b1 = runs[r + q].second;
+                const int v = cur[std::min(k[q - 1], runs[r + q - 1].second - 1)], B0 = cur[b0], nB = (int)(b1 - b0);
+                int first = nB;
+                for (int e = ptr[v]; e < ptr[v + 1]; e++)
+                    if (other[e] >= B0 && other[e] < B0 + nB) first = std::min(first, other[e] - B0);
+                ok = first < nB;
+                k[q] = lead[q] = b0 + (size_t)first;
+            }
+            if (ok) {
+                for (size_t t = a0; t < k[0]; t++) out.push_back(cur[t]);
+                bool left = true;
+                while (left) {
+                    left = false;
+                    for (int q = 0; q < R; q++) {
+                        const size_t end = runs[r + q].second;
+                        for (size_t t = 0; t < take[q] && k[q] < end; t++) out.push_back(cur[k[q]++]);
+                        left = left || k[q] < end;
+                    }
                 }
-                out.insert(out.end(), cur.begin() + b0, cur.begin() + lead);
-                paired = true;
-                r += 2;
+                for (int q = 1; q < R; q++) out.insert(out.end(), cur.begin() + runs[r + q].first, cur.begin() + lead[q]);
+                grouped = true;
+                r += R;
             }
         }
-        if (!paired) {
+        if (!grouped) {
             out.insert(out.end(), cur.begin() + a0, cur.begin() + a1);
             r += 1;
         }
@@ -905,8 +919,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     std::sort(cur.begin(), cur.end());
                     // row pairs on large partitions, with the stash below (1.2M x 80: -2.2 % with 6
                     // columns, 6 tracers -1.2 %)
-                    if (knob("FESOM2_ROWPAIR", large_auto ? 1 : 0))
-                        row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other);
+                    // (tuning: FESOM2_ROWPAIR = R > 1 takes R rows per block)
+                    if (const int rp = knob("FESOM2_ROWPAIR", large_auto ? 1 : 0))
+                        row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other,
+                                  rp > 1 ? rp : 2);
                 }
                 npatch++;
                 order.insert(order.end(), cur.begin(), cur.end());

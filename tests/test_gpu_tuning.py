@@ -74,7 +74,8 @@ SPLIT_KNOBS = [{"FESOM2_ODD_PAIR": "0"}, {"FESOM2_NL_PAIR": "0"}, {"FESOM2_NL_PA
                {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"},
                {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_STASH": "2", "FESOM2_P1V_B3H": "1"},
                {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1", "FESOM2_ROWPAIR": "1"},
-               {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"}]
+               {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"},
+               {"FESOM2_ROWPAIR": "3", "FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1"}]
 
 
 @pytest.mark.parametrize("knobs", SPLIT_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
