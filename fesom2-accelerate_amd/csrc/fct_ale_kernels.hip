@@ -532,10 +532,8 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         flux = m[c] * a.dt * ai[c] - a.eps;
         om[c] = RMIN(1., (tn - lo[c]) / flux);
     }
-    // OPT & 128 (tuning build): plus/minus as plain stores, so the Infinity Cache may keep them
-    // for b3h's gathers
-    stv_s<C, NT && !(OPT & 128)>(a.plus + b, op, nw);
-    stv_s<C, NT && !(OPT & 128)>(a.minus + b, om, nw);
+    stv_s<C, NT>(a.plus + b, op, nw);
+    stv_s<C, NT>(a.minus + b, om, nw);
     }
     if constexpr (VERT) {
         // ---- b3-vertical + c-vertical on the own column (as k_p2: docs/refactoring.md:204-233, :295-300)
@@ -1458,22 +1456,6 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
             }
             if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256, true>), groups, G, S, lds, s, mp, a, G, inv);
             F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256>), groups, G, S, lds, s, mp, a, G, inv);
-        }
-    }
-    // FESOM2_PM_PLAIN = 1: the production forms with plus/minus stored as plain (cache-allocating)
-    // stores, the other single-use streams non-temporal as in the product
-    if (knob("FESOM2_PM_PLAIN", 0) && a.vlimit == 1) {
-        const int L = a.nl - 1;
-        const bool odd = odd_pairs(L);
-        if (odd || levels_per_thread(L) == 2) {
-            const int S = (L + 1) / 2, G = plan_columns(S, mp);
-            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
-            const size_t lds = p1_lds_bytes(G, L, 1, in);
-            const float inv = 1.0f / (float)S;
-            if (odd && in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 128, true>), groups, G, S, lds, s, mp, a, G, inv);
-            if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 128, true>), groups, G, S, lds, s, mp, a, G, inv);
-            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 128>), groups, G, S, lds, s, mp, a, G, inv);
-            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 128>), groups, G, S, lds, s, mp, a, G, inv);
         }
     }
     // FESOM2_P1V_WAVES = W: the production forms held to W waves/SIMD

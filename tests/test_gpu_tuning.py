@@ -68,8 +68,7 @@ SPLIT_KNOBS = [{"FESOM2_ODD_PAIR": "0"}, {"FESOM2_NL_PAIR": "0"}, {"FESOM2_NL_PA
                {"FESOM2_TILE_REV": "7"},
                {"FESOM2_TILE_REV": "6", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_WAVES": "8"},
                {"FESOM2_P2H_BATCH": "6"}, {"FESOM2_P2H_BATCH": "8"},
-               {"FESOM2_PM_PLAIN": "1"}, {"FESOM2_PM_PLAIN": "1", "FESOM2_P1V_B3H": "1", "FESOM2_TILE_REV": "2"},
-               {"FESOM2_B3H_STPLAIN": "1"}, {"FESOM2_B3H_STPLAIN": "1", "FESOM2_PM_PLAIN": "1", "FESOM2_P1V_B3H": "1", "FESOM2_TILE_REV": "5"},
+               {"FESOM2_B3H_STPLAIN": "1"}, {"FESOM2_B3H_STPLAIN": "1", "FESOM2_P1V_B3H": "1", "FESOM2_TILE_REV": "5"},
                {"FESOM2_ROWPAIR": "1"}, {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1"},
                {"FESOM2_ROWPAIR": "1", "FESOM2_P1V_B3H": "1", "FESOM2_PATCH": "100"},
                {"FESOM2_P1V_STASH": "1", "FESOM2_P1V_B3H": "1"}, {"FESOM2_P1V_STASH": "2", "FESOM2_P1V_B3H": "1"},
