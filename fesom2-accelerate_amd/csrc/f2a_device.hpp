@@ -20,18 +20,26 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 
 // Bijective XCD-aware swizzle: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // residue class a contiguous range of tiles.  Speed only, never correctness.
-static __constant__ int c_xcd_swizzle = 1;  // FESOM2_XCD=0 disables (A/B measurements, tuning build)
-// FESOM2_ABLATE (tuning build, timing-only experiments, results are wrong): bit 0 skips the cluster
-// gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2.
-static __constant__ int c_ablate = 0;
-// FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile order
-static __constant__ int c_tracer_major = 2;  // measured: b3h tracer-slowest, p1/p2 tracer-fastest
-// FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range backwards, so it
-// starts on the data the previous kernel touched last (still in the Infinity Cache)
+// The switches below are compile-time constants in the product build (their measured defaults) and
+// __constant__ knobs only in the tuning build (F2A_TUNING, `make tuning`):
+//   c_xcd_swizzle   FESOM2_XCD=0 disables the swizzle (A/B measurements)
+//   c_ablate        FESOM2_ABLATE, timing-only experiments (results are wrong): bit 0 skips the cluster
+//                   gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2
+//   c_tracer_major  FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile
+//                   order; measured: b3h tracer-slowest, p1/p2 tracer-fastest
+//   c_tile_rev      FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range
+//                   backwards, so it starts on the data the previous kernel touched last (still in the
+//                   Infinity Cache); the product takes the direction per call (Tracers::order)
 #if F2A_TUNING
+static __constant__ int c_xcd_swizzle = 1;
+static __constant__ int c_ablate = 0;
+static __constant__ int c_tracer_major = 2;
 static __constant__ int c_tile_rev = 0;
 #else
-static constexpr int c_tile_rev = 0;  // the product walks every range forwards
+static constexpr int c_xcd_swizzle = 1;
+static constexpr int c_ablate = 0;
+static constexpr int c_tracer_major = 2;
+static constexpr int c_tile_rev = 0;
 #endif
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
@@ -310,6 +318,10 @@ __device__ __forceinline__ void st1_s(real *__restrict__ p, real v)
     else *p = v;
 }
 
+// the level count an EdgeRef::code carries (bits 1..11; bit 0 = second endpoint, bits 12 and up the
+// LDS-stash slot of a block-internal edge, see kStashShift): every decode goes through here
+__device__ __forceinline__ int edge_lev(int code) { return (code >> 1) & kLevMask; }
+
 // tvert(n, z): max/min over the elements around n of UV_rhs(e, z) (reference.cpp:358-378), taken
 // straight from ttf/LO over the node's cluster (a1 + a2 + the cluster part of a3, see RingRef).
 // (vx, vn must be initialised by the caller: -/+bignumber where an adjacent element is dry, else
@@ -372,28 +384,28 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
         real h[kBatch][C];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            if (z0 < ((code[k] >> 1) & kLevMask)) {
+            if (z0 < edge_lev(code[k])) {
                 ldo_pre<C, ODD>(adf_h + idx[k], h[k], last1);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; c++) h[k][c] = 0.;
             }
         }
-        if (stash) {  // tuning (FESOM2_P1V_STASH): the block-internal edges' raw flux into LDS
+        if (stash) {  // (large partitions; OPT & 256 of k_p1) the block-internal edges' raw flux into LDS
 #pragma unroll
             for (int k = 0; k < kBatch; k++) {
                 const int sl = code[k] >> kStashShift;
                 if (sl)
 #pragma unroll
                     for (int c = 0; c < C; c++)
-                        if (z0 + c < ((code[k] >> 1) & kLevMask)) stash[(sl - 1) * L + z0 + c] = h[k][c];
+                        if (z0 + c < edge_lev(code[k])) stash[(sl - 1) * L + z0 + c] = h[k][c];
             }
         }
 #pragma unroll
         for (int k = 0; k < kBatch; k++)
 #pragma unroll
             for (int c = 0; c < C; c++)
-                if (z0 + c < ((code[k] >> 1) & kLevMask)) f(c, h[k][c], code[k] & 1);
+                if (z0 + c < edge_lev(code[k])) f(c, h[k][c], code[k] & 1);
     }
 }
 
@@ -414,7 +426,7 @@ __device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ ed
         real h[kBatch][C], po[kBatch][C], mo[kBatch][C];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            if (z0 < ((er[k].code >> 1) & kLevMask)) {
+            if (z0 < edge_lev(er[k].code)) {
                 ldo<C, ODD>(adf_h + (size_t)er[k].edge * L + z0, h[k], last1);
                 ldo<C, ODD>(plus + (size_t)er[k].other * L + z0, po[k], last1);
                 ldo<C, ODD>(minus + (size_t)er[k].other * L + z0, mo[k], last1);
@@ -422,7 +434,7 @@ __device__ __forceinline__ void for_edges_limited(const EdgeRef *__restrict__ ed
         }
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            const int lev = (er[k].code >> 1) & kLevMask, second = er[k].code & 1;
+            const int lev = edge_lev(er[k].code), second = er[k].code & 1;
 #pragma unroll
             for (int c = 0; c < C; c++) {
                 if (z0 + c >= lev) continue;

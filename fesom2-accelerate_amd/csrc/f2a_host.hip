@@ -127,6 +127,7 @@ Buffer *allocate(void *host, size_t bytes, bool create_event)
 bool h2d(Buffer *b, bool sync, hipStream_t s, bool record)
 {
     if (!b->host_pointer || !b->size) return true;
+    b->version++;
     if (sync) return ok(hipMemcpy(b->device_pointer, b->host_pointer, b->size, hipMemcpyHostToDevice), "H2D");
     if (!ok(hipMemcpyAsync(b->device_pointer, b->host_pointer, b->size, hipMemcpyHostToDevice, s), "H2D async"))
         return false;
@@ -681,6 +682,54 @@ PlanShape plan_shape(bool batched)
     return s;
 }
 
+long long large_partition_cells()
+{
+    // plan option FESOM2_LARGE_CELLS (read when a plan is built): owned wet cells from which the
+    // large-partition rules apply
+    const char *v = getenv("FESOM2_LARGE_CELLS");
+    return v ? std::max(0ll, atoll(v)) : (32ll << 20);
+}
+
+ResolvedShape resolve_shape(const PlanShape &shape, long long wet_cells, int nl)
+{
+    ResolvedShape r;
+    const bool large = wet_cells >= large_partition_cells();
+    // explicit columns per block: every column-group kernel must fit 1024 threads with its widest
+    // shape (one level per thread: nl - 1 slots)
+    r.gcols = (shape.gcols > 0 && shape.gcols * (nl - 1) <= 1024) ? shape.gcols : 0;
+    r.gshift = r.gcols ? 0 : shape.gshift;
+    if (r.gshift == PlanShape::kAuto) {
+        // a large partition (>= 32M owned wet cells): smaller blocks -- the largest column count below
+        // the natural one that keeps >= 90 % of the block's lanes busy -- taken in row pairs with
+        // the stash.  Measured, 6 tracers at 1.2M x 80 (40 slots; 8 columns natural), one box, 3
+        // interleaved rounds: 6 columns (240 of 256 lanes) 21.26 ms, 3: 21.52-21.67, 12: 21.65, 4:
+        // 21.76, 7: 23.15, 8: 23.0-23.3; with row pairs + stash 6 columns 21.24, 4: 22.05, 8: 22.43.
+        // One tracer: 6 columns in row pairs with the stash 4.06 ms against 4.14-4.17 with 8 in
+        // single rows (-2.2 %), 6 columns alone -0.4 %.  On 127k x 47 (6M cells) every smaller
+        // block loses (5 columns: +1.6 %, 7: +0.6 %): small partitions keep the natural one.
+        r.gshift = 0;
+        if (large) {
+            r.large = true;
+            const int S = p1v_slots(nl), Gn = p1v_group_columns(nl, 0);
+            for (int g = Gn - 1; g >= 1; g--)
+                if (10 * g * S >= 9 * ((g * S + 63) / 64 * 64) && g * (nl - 1) <= 1024) {
+                    r.gcols = g;
+                    break;
+                }
+        }
+    }
+    // nodes per patch: the shape's (plan options FESOM2_PATCH / FESOM2_BATCH_PATCH), else by
+    // numbering (build_plan); the batched plan's default: 4096 when its blocks are smaller
+    // (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer plan's choice
+    // (127k x 47: 16384 best)
+    r.patch = shape.patch == PlanShape::kAuto ? (r.gshift < 0 || r.gcols ? 4096 : 0) : shape.patch;
+    // FESOM2_P1V_B3H: 1 on, 0 off, unset: on for large partitions -- measured 1.2M x 80 (96M
+    // cells) -3.5 % per pass, 127k x 47 (6M cells, latency-bound) +2 %
+    const char *ienv = getenv("FESOM2_P1V_B3H");
+    r.internal = ienv ? atoi(ienv) != 0 : large;
+    return r;
+}
+
 std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
                                  int n_csr, int nl, const PlanShape &shape, std::string &err)
 {
@@ -695,37 +744,15 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     d.n_total = n_total;
     d.n_edges = n_edges;
     d.nl = nl;
-    d.gshift = shape.gshift;
-    // explicit columns per block: every column-group kernel must fit 1024 threads with its widest
-    // shape (one level per thread: nl - 1 slots)
-    d.gcols = (shape.gcols > 0 && shape.gcols * (nl - 1) <= 1024) ? shape.gcols : 0;
-    if (d.gcols) d.gshift = 0;
-    long long wet_cells = 0;  // owned wet cells (the size rules below and FESOM2_P1V_B3H)
+    long long wet_cells = 0;  // owned wet cells (the size rules of resolve_shape)
     if (m.nlev_nod)
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
-    // a large partition: smaller blocks (below), row-pair blocks and the internal edges' raw flux
-    // kept in LDS (row_pairs, MeshPlanDev::int_stash; tuning: FESOM2_ROWPAIR, FESOM2_P1V_STASH)
-    bool large_auto = false;
-    if (d.gshift == PlanShape::kAuto) {
-        // a large partition (>= 32M owned wet cells): smaller blocks -- the largest column count below
-        // the natural one that keeps >= 90 % of the block's lanes busy -- taken in row pairs with
-        // the stash (below).  Measured, 6 tracers at 1.2M x 80 (40 slots; 8 columns natural), one
-        // box, 3 interleaved rounds: 6 columns (240 of 256 lanes) 21.26 ms, 3: 21.52-21.67, 12:
-        // 21.65, 4: 21.76, 7: 23.15, 8: 23.0-23.3; with row pairs + stash 6 columns 21.24, 4: 22.05,
-        // 8: 22.43.  One tracer: 6 columns in row pairs with the stash 4.06 ms against 4.14-4.17
-        // with 8 in single rows (-2.2 %), 6 columns alone -0.4 %.  On 127k x 47 (6M cells) every
-        // smaller block loses (5 columns: +1.6 %, 7: +0.6 %): small partitions keep the natural one.
-        d.gshift = 0;
-        if (wet_cells >= (32ll << 20)) {
-            large_auto = true;
-            const int S = p1v_slots(nl), Gn = p1v_group_columns(nl, 0);
-            for (int g = Gn - 1; g >= 1; g--)
-                if (10 * g * S >= 9 * ((g * S + 63) / 64 * 64) && g * (nl - 1) <= 1024) {
-                    d.gcols = g;
-                    break;
-                }
-        }
-    }
+    const ResolvedShape rs = resolve_shape(shape, wet_cells, nl);
+    d.gshift = rs.gshift;
+    d.gcols = rs.gcols;
+    // a large partition: smaller blocks, row-pair blocks and the internal edges' raw flux kept in
+    // LDS (row_pairs, MeshPlanDev::int_stash; tuning: FESOM2_ROWPAIR, FESOM2_P1V_STASH)
+    const bool large_auto = rs.large;
     const int L = nl - 1;
     char msg[256];
     auto fail = [&](const char *s) {
@@ -856,8 +883,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // FESOM2_BATCH_PATCH), else by numbering; the batched plan's default: 4096 when its blocks
         // are smaller (measured 1024..16384 at 6 x 1.2M x 80), else the single-tracer
         // plan's choice (127k x 47: 16384 best)
-        const int sp = shape.patch == PlanShape::kAuto ? (d.gshift < 0 || d.gcols ? 4096 : 0) : shape.patch;
-        const int patch = sp > 0 ? sp : (local_numbering ? 16384 : 4096);
+        const int patch = rs.patch > 0 ? rs.patch : (local_numbering ? 16384 : 4096);
         // order inside a patch: ascending index (0) or Cuthill-McKee (1); FESOM2_PATCH_ORDER in the
         // tuning build
         const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);
@@ -977,8 +1003,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         d.n_edge_interior = (int)std::count_if(einfo.begin(), einfo.end(), interior_edge);
         // FESOM2_P1V_B3H: 1 on, 0 off, unset: on from 32M owned wet cells per GPU -- measured
         // 1.2M x 80 (96M cells) -3.5 % per pass, 127k x 47 (6M cells, latency-bound) +2 %
-        const char *ienv = getenv("FESOM2_P1V_B3H");
-        if (ienv ? atoi(ienv) != 0 : wet_cells >= (32ll << 20)) {
+        if (rs.internal) {
             const int IG = p1v_group_columns(nl, d.gshift, d.gcols);
             std::vector<int> pos(n_owned);
             for (int k = 0; k < n_owned; k++) pos[order[k]] = k;
@@ -1095,7 +1120,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
 namespace {
 using PlanKey = std::tuple<const void *, const void *, const void *, const void *, const void *,
                            const void *, const void *, int, int, int, int, int, bool>;
-std::map<PlanKey, std::unique_ptr<Plan>> g_plans;
+std::map<PlanKey, std::shared_ptr<Plan>> g_plans;
 
 template <class T>
 std::vector<T> fetch(Buffer *b, size_t count)
@@ -1158,16 +1183,33 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
         m.nie_num = nnum.data();
         m.dim = h.dim;
     }
+    // a batched call whose shape resolves like the single-tracer one shares that plan (one build,
+    // one set of device arrays; a graph capture after fesom2_prepare_mesh_ finds it either way)
+    bool share = false;
+    PlanKey skey = key;
+    if (batched) {
+        long long wet = 0;
+        for (int v : nln) wet += std::max(v - 1, 0);
+        share = resolve_shape(plan_shape(true), wet, nl) == resolve_shape(plan_shape(false), wet, nl);
+        std::get<12>(skey) = false;
+        if (share) {
+            auto si = g_plans.find(skey);
+            if (si != g_plans.end()) {
+                g_plans[key] = si->second;
+                return si->second.get();
+            }
+        }
+    }
     std::string err;
-    auto plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, plan_shape(batched), err);
+    std::shared_ptr<Plan> plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, plan_shape(batched && !share), err);
     if (!plan) {
         report("invalid mesh: %s", err.c_str());
         return nullptr;
     }
     plan->serial = track_object(plan.get());
-    const Plan *p = plan.get();
-    g_plans[key] = std::move(plan);
-    return p;
+    g_plans[key] = plan;
+    if (share) g_plans[skey] = plan;
+    return plan.get();
 }
 
 

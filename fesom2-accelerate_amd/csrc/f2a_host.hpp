@@ -199,6 +199,27 @@ struct PlanShape {
 // FESOM2_PATCH / FESOM2_BATCH_PATCH and FESOM2_BATCH_GROUP_SHIFT (read when the plan is built)
 PlanShape plan_shape(bool batched);
 
+// A shape with the automatic rules applied for a partition of `wet_cells` owned wet cells.  The
+// large-partition rules (smaller blocks in row pairs, the internal edges' LDS stash, the
+// block-internal edges limited in p1v) start at large_partition_cells() = 32M wet cells; the plan
+// option FESOM2_LARGE_CELLS moves that threshold (tests run the large plan on small meshes with
+// it).  Two shapes that resolve alike give the same plan: get_plan then shares one plan between
+// single-tracer and batched calls (every partition below the threshold).
+struct ResolvedShape {
+    int patch = 0;          // nodes per BFS patch, 0: by numbering (16384 / 4096), 1: index order
+    int gshift = 0;         // MeshPlanDev::gshift
+    int gcols = 0;          // MeshPlanDev::gcols (0: natural column count << gshift)
+    bool large = false;     // row pairs + LDS stash (automatic shape on a large partition)
+    bool internal = false;  // block-internal edges limited in p1v (FESOM2_P1V_B3H forces it)
+    bool operator==(const ResolvedShape &o) const
+    {
+        return patch == o.patch && gshift == o.gshift && gcols == o.gcols && large == o.large &&
+               internal == o.internal;
+    }
+};
+long long large_partition_cells();
+ResolvedShape resolve_shape(const PlanShape &s, long long wet_cells, int nl);
+
 // Node->edge CSR for nodes [0, n_csr) in ascending edge order; clusters for [0, n_owned) when the
 // element connectivity is present.  Validates every index; returns nullptr with `err` set.
 std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, int n_edges,
@@ -210,7 +231,8 @@ struct MeshHandles {
     int dim = 0;
 };
 // Cached per (handles, partition sizes, batched); built synchronously on first use.  `batched`: the
-// plan of calls with ntracers > 1 (PlanShape).
+// plan of calls with ntracers > 1 (PlanShape) -- the single-tracer plan itself (one object under
+// both keys) when the two shapes resolve alike (ResolvedShape).
 const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges, int nl,
                      bool with_ring, bool batched = false);
 void drop_plans_of(const Buffer *b);

@@ -53,6 +53,7 @@ struct Buffer {
     hipEvent_t event = nullptr;
     bool has_event = false;
     uint64_t serial = 0;  // live-object serial (track_object): graph replays check it is unchanged
+    uint64_t version = 0;  // bumped by every host -> device upload through the library (h2d, fesom2_upload_)
     // phase mark (f2a_host.hpp): on fct_adf_h the mesh plan whose block-internal edges a p1v launch
     // limited (the phase-2 entry then limits the others), on fct_adf_v the plan whose phase-1 launch
     // did b3-vertical; cleared by the entry that finishes the phase and by every upload

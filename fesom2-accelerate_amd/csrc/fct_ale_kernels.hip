@@ -163,13 +163,13 @@ __global__ __launch_bounds__(kBlock) void k_b1h(MeshPlanDev mp, int L, const rea
     const int lane = threadIdx.x & 63;
     const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
     int lmax = 0;
-    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].code >> 1);
+    for (int k = e0; k < e1; k++) lmax = max(lmax, edge_lev(mp.edges[k].code));
     const size_t b = (size_t)n * L;
     for (int z = lane; z < lmax; z += kWave) {
         real p = plus[b + z], m = minus[b + z];
         for (int k = e0; k < e1; k++) {
             const EdgeRef er = mp.edges[k];
-            if (z < (er.code >> 1)) {
+            if (z < edge_lev(er.code)) {
                 const real h = adf_h[(size_t)er.edge * L + z];
                 if (er.code & 1) {
                     p += RMAX(0., -h);
@@ -288,14 +288,14 @@ __global__ __launch_bounds__(kBlock) void k_ch(MeshPlanDev mp, int L, const real
     const int lane = threadIdx.x & 63;
     const int e0 = mp.edge_ptr[n], e1 = mp.edge_ptr[n + 1];
     int lmax = 0;
-    for (int k = e0; k < e1; k++) lmax = max(lmax, mp.edges[k].code >> 1);
+    for (int k = e0; k < e1; k++) lmax = max(lmax, edge_lev(mp.edges[k].code));
     const size_t b = (size_t)n * L, a = (size_t)n * (L + 1);
     for (int z = lane; z < lmax; z += kWave) {
         const real dta = dt / area[a + z];
         real d = del_h[b + z];
         for (int k = e0; k < e1; k++) {
             const EdgeRef er = mp.edges[k];
-            if (z < (er.code >> 1)) {
+            if (z < edge_lev(er.code)) {
                 const real h = adf_h[(size_t)er.edge * L + z];
                 d = (er.code & 1) ? d - h * dta : d + h * dta;
             }
@@ -365,8 +365,9 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     // (behind the records and the internal-edge staging: p1_lds_bytes)
     real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
-    // OPT & 256 (tuning, FESOM2_P1V_STASH, with OPT & 16): the internal edges' raw flux, kept by
-    // the first endpoint's b1h gather ([slot][level], behind every other region)
+    // OPT & 256 (with OPT & 16; the product default on large partitions, MeshPlanDev::int_stash; the
+    // tuning build's FESOM2_P1V_STASH forces it): the internal edges' raw flux, kept by the first
+    // endpoint's b1h gather ([slot][level], behind every other region)
     real *stash = nullptr;
     if constexpr (VERT && (OPT & 16) && (OPT & 256))
         stash = cmx + (VLIMIT != 1 ? G * L : 0);

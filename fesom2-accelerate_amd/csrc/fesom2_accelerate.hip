@@ -968,7 +968,13 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
     mh.dim = *nod_in_elem2D_dim;
     if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !bnlnod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
     mh.nlev_nod = bnlnod;
-    if (get_plan(mh, N, NT, E, *nl, true) && get_plan(mh, N, NT, E, *nl, false)) *istat = 0;
+    // every plan a call on this mesh may ask for: single-tracer and batched (the same object where
+    // their shapes resolve alike), with and without the element ring -- so a graph capture of any
+    // entry sequence after this call builds nothing
+    for (const bool batched : {false, true})
+        for (const bool ring : {true, false})
+            if (!get_plan(mh, N, NT, E, *nl, ring, batched)) return;
+    *istat = 0;
 }
 
 // Diagnostics of the mesh plan the phase-1 kernels run on (for the benchmark's byte counts):
@@ -1042,6 +1048,7 @@ void fesom2_upload_(void **mem, void *host_ptr, int *istat)
 {
     Buffer *b = buf(mem, "fesom2_upload_");
     if (b) mark_internal(b, nullptr, nullptr);  // new contents
+    if (b) b->version++;
     *istat = (b && ok(hipMemcpy(b->device_pointer, host_ptr, b->size, hipMemcpyHostToDevice), "H2D")) ? 0 : 1;
 }
 

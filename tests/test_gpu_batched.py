@@ -309,6 +309,82 @@ def test_batched_plan_of_a_large_partition():
         dm.free()
 
 
+@pytest.mark.parametrize("ntr", [1, 3])
+@pytest.mark.parametrize("mesh", ["odd L", "variable depth", "delaunay hilbert", "permuted"])
+def test_large_partition_plan_on_small_meshes(mesh, ntr, monkeypatch):
+    """The product's large-partition plan (6-column blocks in row pairs, the internal edges' raw
+    flux stashed in LDS, the block-internal edges limited inside p1v) on meshes the 1.2M x 80 runs
+    never reach: odd L (the k_p1<..., 52 | 256, true> form), variable depth, an unstructured
+    Delaunay mesh with Hilbert numbering and a scattered numbering.  FESOM2_LARGE_CELLS=0 moves the
+    32M-cell threshold so small meshes take that plan; split and fused pairs exact."""
+    monkeypatch.setenv("FESOM2_LARGE_CELLS", "0")
+    if mesh == "odd L":
+        m = synth.make_mesh(64, 40, 48, full_depth=True)
+    elif mesh == "variable depth":
+        m = synth.make_mesh(64, 40, 81)
+    elif mesh == "delaunay hilbert":
+        m = synth.delaunay_mesh(3000, 48, numbering="hilbert")
+    else:
+        m = synth.permute_mesh(synth.make_mesh(64, 40, 48))
+    tracers = synth.make_tracer_fields(m, ntr)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers) if ntr > 1 else engine.FctAle(dm, tracers[0])
+    try:
+        info = dm.info(batched=ntr > 1)
+        assert info["internal_edges"] > 0, info
+        # the largest column count below the natural one with >= 90 % of the lanes busy: 47 levels
+        # (24 slots, 8 columns natural) -> 5, 80 levels (40 slots, 8 natural) -> 6
+        assert info["p1v_columns"] == {47: 5, 80: 6}[m.L], info
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        wants = [O.full_pass(m, t) for t in tracers]
+        got = {k: e.download(k).reshape(ntr, -1) for k in ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")}
+        for k in range(ntr):
+            assert_cols_equal(got["plus"][k][: m.N * m.L], wants[k]["plus"][: m.N * m.L], m.nlev_nod, m.L, m.N,
+                              f"plus[{k}]")
+            for name, n in (("adf_v", m.N * m.nl), ("del_v", m.N * m.L), ("del_h", m.N * m.L), ("adf_h", m.E * m.L)):
+                bad = np.flatnonzero(got[name][k][:n] != wants[k][name][:n])
+                assert bad.size == 0, f"{mesh} {name}[{k}]: {bad.size} differ, first at {bad[:5]}"
+    finally:
+        e.free()
+        dm.free()
+
+
+def test_batched_graph_after_prepare_only():
+    """A batched pass captured right after fesom2_prepare_mesh_ (no eager call first): prepare builds
+    the batched plans too (or shares the single-tracer one where the shapes resolve alike), so the
+    capture builds nothing."""
+    m = synth.config_mesh("8k x 20")
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    dm.prepare()
+    e = engine.FctAleBatch(dm, tracers)
+    graph = None
+    try:
+        with abi.Graph.capture(e.stream) as graph:
+            assert e.pre_comm_v() == 7, abi.last_error()
+            assert e.post_comm_h() == 9, abi.last_error()
+        graph.launch(e.stream)
+        e.sync()
+        for k in range(3):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+        # the same with the fused batched pair
+        for name in ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h"):
+            e.upload(name)
+        graph.free()
+        with abi.Graph.capture(e.stream) as graph:
+            assert e.full_pass() == 9, abi.last_error()
+        graph.launch(e.stream)
+        e.sync()
+        for k in range(3):
+            check_tracer(m, e, k, O.full_pass(m, tracers[k]))
+    finally:
+        if graph is not None:
+            graph.free()
+        e.free()
+        dm.free()
+
 
 @pytest.mark.parametrize("env,expect", [(None, {1: 13, 2: 0, 6: 0}), ("0", {1: 0, 2: 0, 6: 0}),
                                         ("1", {1: 13, 2: 13, 6: 13})])
