@@ -112,6 +112,19 @@ void transfer_var_async_(void **mem, real *host_ptr, void **stream, bool *record
     h2d(b, false, stream_of(stream), record_event && *record_event);
 }
 
+void fesom2_transfer_back_async_(void **mem, real *host_ptr, void **stream, int *istat)
+{
+    *istat = 1;
+    Buffer *b = buf(mem, "fesom2_transfer_back_async_");
+    if (!b) return;
+    if (!host_ptr) {
+        report("fesom2_transfer_back_async_: no host array");
+        return;
+    }
+    b->host_pointer = host_ptr;
+    if (d2h_async(b, stream_of(stream))) *istat = 0;
+}
+
 void make_stream_(void **stream, int *istat)
 {
     *istat = 0;

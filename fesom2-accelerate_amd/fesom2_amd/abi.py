@@ -33,6 +33,7 @@ EXPORTS = (
     "fesom2_alloc_var_i8_", "fesom2_reserve_var_i8_", "fct_ale_pre_comm_v_acc_", "fct_ale_post_comm_h_acc_",
     "fesom2_graph_begin_", "fesom2_graph_end_", "fesom2_graph_launch_", "fesom2_graph_free_",
     "fesom2_graph_info_", "fesom2_mesh_info_", "fesom2_bind_c_vertical_", "fesom2_pass_order_",
+    "fesom2_transfer_back_async_",
 )
 
 # the reference's C++ convenience entries (include/fesom2-accelerate-legacy.hpp: C linkage, plain

@@ -41,6 +41,12 @@ module fesom2_accelerate
       real(c_double) :: host(*)
       logical(c_bool) :: record_event
     end subroutine
+    subroutine fesom2_transfer_back_async(handle, host, stream, istat) bind(C, name="fesom2_transfer_back_async_")
+      import :: c_ptr, c_double, c_int
+      type(c_ptr) :: handle, stream
+      real(c_double) :: host(*)
+      integer(c_int) :: istat
+    end subroutine
     subroutine make_stream(stream, istat) bind(C, name="make_stream_")
       import :: c_ptr, c_int
       type(c_ptr) :: stream

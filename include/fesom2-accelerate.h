@@ -173,6 +173,14 @@ void fesom2_pass_order_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDi
 /* Copy a handle's device contents to/from a host array (no rebinding), synchronous. */
 void fesom2_download_(void **mem, void *host_ptr, int *istat);
 void fesom2_upload_(void **mem, void *host_ptr, int *istat);
+/* Asynchronous device -> host copy of a handle on *stream: the mirror of transfer_var_async_ and
+ * of the reference's asynchronous transfer_back (src/fesom2-accelerate.cu:230-253, which only the
+ * phase entries call).  Rebinds the handle's host pointer to host_ptr (as transfer_var_async_
+ * does) and enqueues the copy; the host awaits the stream (await_stream_) before reading it.
+ * For a device-resident host (fesom2_set_resident_(1)) that uploads the producer's fields itself
+ * and takes back only what it needs (e.g. del_ttf_advvert / del_ttf_advhoriz after the c-step).
+ * istat 0 = ok. */
+void fesom2_transfer_back_async_(void **mem, real_type *host_ptr, void **stream, int *istat);
 /* Release a handle / stream / pinned buffer (the reference never frees). */
 void fesom2_free_(void **mem);
 void fesom2_free_stream_(void **stream);
