@@ -28,12 +28,19 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
             exchange); a mismatch exits with status 1.
 * extra     (default --extras auto) further BASELINE configs in the same run, each with its own
             timing, roofline and check: at N = 1 configs[1] (127k x 47, 1 and 6 tracers), configs[3]
-            (1.2M x 80, 6 tracers batched) and configs[4]'s strong-scaling base (9.6M x 80 on one
-            GPU); at N > 1 the strong-scaling leg (9.6M x 80 split over the N GPUs).  Every N > 1
-            record carries the per-rank spread of step times and the halo exchange's own time and
-            hidden fraction.
+            (1.2M x 80, 6 tracers batched), configs[4]'s strong-scaling base (9.6M x 80 on one GPU)
+            and one rank's share of its N = 8 point (an interior strip of the 8-way split, no
+            exchange), and SURVEY.md 8(d)'s transfer-inclusive rates at 1.2M x 80 (the reference
+            transfer semantics; the producer-upload mode with two tracers on two streams), each
+            against a same-run PCIe probe; at N > 1 the strong-scaling leg (9.6M x 80 split over
+            the N GPUs).  Every N > 1 record carries the per-rank spread of step times and the halo
+            exchange's own time and hidden fraction.
+* ceilings  pass_roofline.frac_of_copy: the pass's survey bytes per second against a flat 16-B copy
+            on this GPU in this run; roofline.frac_of_copy / frac_of_p1v_pattern: the dominant
+            kernel's against the copy and against p1v's own stream pattern (one tracer's, or the
+            batch's for a batched leg) -- tools/stream_probe.hip, child processes run first.
 * cpu_baseline  the oracle's single-threaded full pass (bit-identical to reference.cpp for a1..b2)
-            on the same mesh, rank 0 at N = 1 only; plus "all_cores": P single-threaded oracle
+            on the same mesh, rank 0 at N = 1 only; plus "per_gpu_share": P single-threaded oracle
             processes on a P-way strip partition of the same mesh (MPI-style replicas, SURVEY.md
             8(d)), run before this process touches the GPU.
 * watchdog  a thread per rank: RCCL communicator setup, the first exchange step and each leg have a
@@ -125,6 +132,20 @@ def kernel_bytes(s, ntr=1, split=False):
             "pass": p1 + b3h + p2, "pass_split": p1v + b3h + p2h, "survey_pass": survey}
 
 
+def pass_roofline(survey_bytes, ms_step, ceiling=None):
+    """The whole pass against the HBM peak on SURVEY.md 8(d)'s bytes, and (frac_of_copy) against what
+    a flat 16-B copy moves on this GPU in this run (``ceiling``: stream_ceiling's record) -- the
+    figure that compares across rounds and boxes."""
+    gbs = survey_bytes / (ms_step * 1e-3) / 1e9
+    out = {"alg_bytes": survey_bytes, "GBps": round(gbs, 1), "frac": round(gbs / (HBM_PEAK / 1e9), 4),
+           "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass; frac_of_copy: "
+                   "the same against a flat 16-B copy on this GPU in this run (tools/stream_probe.hip)"}
+    if ceiling and ceiling.get("copy_GBps"):
+        out["copy_GBps"] = ceiling["copy_GBps"]
+        out["frac_of_copy"] = round(gbs / ceiling["copy_GBps"], 4)
+    return out
+
+
 def reference_byte_models(m):
     """The reference's own per-kernel byte models -- what its kernel_tuner scripts divide by the
     kernel time to print GB/s -- evaluated on this mesh, for the one-kernel-per-step
@@ -194,33 +215,52 @@ def _cpu_replica(job):
     return int((m.nlev_nod[: m.N].astype(np.int64) - 1).sum()), best, reps
 
 
-def cpu_all_cores(args, pool, P, budget=4.0):
-    """P concurrent single-threaded oracle processes on a P-way partition of the workload mesh;
-    value = all owned cells / the slowest replica's best pass."""
+def cpu_per_gpu_share(args, pool, P, budget=4.0):
+    """P concurrent single-threaded oracle processes on a P-way partition of the workload mesh --
+    P = this GPU's share of the host's cores (16 of a 128-core, 8-GPU node; the worker pool's size,
+    make_pool) -- plus the whole host extrapolated linearly from them (the replicas share nothing, so
+    the full node would run physical_cores of them at the same per-core rate; not measured here: the
+    GPU box's other seven GPUs' jobs own the other cores).  value = all owned cells / the slowest
+    replica's best pass."""
     jobs = [(args.config, not args.parity_levels, P, p, budget) for p in range(P)]
     res = pool.map(_cpu_replica, jobs)
     cells = sum(r[0] for r in res)
     slowest = max(r[1] for r in res)
-    return {"value": round(cells / slowest, 1), "unit": "cell-updates/s", "cores": P,
+    value = cells / slowest
+    phys = host_info()["physical_cores"]
+    return {"value": round(value, 1), "unit": "cell-updates/s", "cores": P,
+            "represents": f"this GPU's share of the host: {P} of {phys or '?'} physical cores, one MPI-style "
+                          f"oracle replica per core",
             "sample": f"{P} concurrent single-threaded oracle processes, y-strip partition of the same "
                       f"{args.config} mesh (one-ring halo each), slowest replica's best of >= "
-                      f"{min(r[2] for r in res)} passes ({slowest:.3f} s/pass)"}
+                      f"{min(r[2] for r in res)} passes ({slowest:.3f} s/pass)",
+            "full_host_estimate": {"value": round(value * phys / P, 1) if phys else None, "cores": phys,
+                                   "unit": "cell-updates/s",
+                                   "method": f"per-core rate of the {P} measured replicas x the host's physical "
+                                             f"cores (linear: independent replicas; an estimate, not measured)"}}
 
 
-def stream_ceiling(args):
+def stream_ceiling(config, tracers=0):
     """The chip's streaming rates measured on this GPU right now (tools/stream_probe.hip, a child
-    process): a flat 16-B copy, and p1v's own 11-read/4-write stream pattern in its block shape
-    without gathers or arithmetic.  None when the probe is not built or fails."""
+    process) at ``config``'s size: a flat 16-B copy, p1v's own 11-read/4-write stream pattern in its
+    block shape without gathers or arithmetic (odd L: its slot shape), and with ``tracers`` > 1 (even
+    L) the batched pattern of the batched plan's 6-column blocks, tiles tracer-fastest
+    (``batch_GBps[str(tracers)]``).  None when the probe is not built or fails."""
     import subprocess
     exe = os.path.join(ROOT, "tools", "stream_probe")
     if not os.path.exists(exe):
         return None
-    nx, ny, nl = synth.CONFIGS[args.config]
+    nx, ny, nl = synth.CONFIGS[config]
     try:
-        out = subprocess.run([exe, str(nx * ny), str(nl - 1), "--json"], capture_output=True, text=True,
-                             timeout=120, check=True).stdout
-        return json.loads(out.strip().splitlines()[-1])
-    except (subprocess.SubprocessError, OSError, ValueError, IndexError):
+        cmd = [exe, str(nx * ny), str(nl - 1), "--json"] + ([str(tracers)] if tracers > 1 else [])
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=180, check=True).stdout
+        lines = [json.loads(ln) for ln in out.strip().splitlines() if ln.startswith("{")]
+        res = dict(lines[-1])
+        res["batch_GBps"] = {str(d["tracers"]): d["batch_GBps"] for d in lines[:-1]
+                             if d.get("G") == 6 and d.get("order") == "tracer-fastest"}
+        res["config"] = config
+        return res
+    except (subprocess.SubprocessError, OSError, ValueError, IndexError, KeyError):
         return None
 
 
@@ -231,7 +271,23 @@ def host_info():
             model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "cpu_model": model}
+    phys = set()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            pid = cid = None
+            for ln in fh:
+                if ln.startswith("physical id"):
+                    pid = ln.split(":", 1)[1].strip()
+                elif ln.startswith("core id"):
+                    cid = ln.split(":", 1)[1].strip()
+                elif not ln.strip():
+                    if cid is not None:
+                        phys.add((pid, cid))
+                    pid = cid = None
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "physical_cores": len(phys) or None,
+            "usable_cores": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
 # ----------------------------------------------------------------------------- watchdog
@@ -290,6 +346,11 @@ def delaunay(args, npts, nl):
 def build_local(args, rank, world):
     """This rank's local mesh (owned y-strip + one-ring halo, built from the strip alone:
     partition.strip_local_mesh) and its exchange lists."""
+    em = getattr(args, "emulate", None)
+    if em:  # one rank's strip of a world-way strong split, on this single GPU (halo from global ids)
+        if world > 1 or args.scaling != "strong" or args.mesh != "structured":
+            raise SystemExit("--emulate-rank: 1 GPU, --scaling strong, structured mesh")
+        rank, world = em
     nx, ny, nl = global_dims(args, world)
     if args.mesh != "structured":
         if world > 1:
@@ -463,15 +524,25 @@ def run_check_pass(args, e, step, m, ntr):
     abi.device_sync()
 
 
-def verify_parallel(args, ctx, e, step, m, world, rank):
+def verify_parallel(args, ctx, e, step, m, world, rank, check_pass=None, fetch=None):
     """The reference harness's verify-before-report (kernels/fct_ale_b2.py:97-100, ``answer=``) for the
     structured meshes: one pass on pristine inputs, the outputs downloaded into memory-mapped files,
     then ctx.pool's workers check row strips of this rank's domain (_check_strip); counts are summed
-    over the strips and over the ranks."""
+    over the strips and over the ranks.  ``check_pass()`` replaces the default pristine pass and
+    ``fetch(name, out)`` the download of all tracers' output ``name`` (the transfer legs: outputs in
+    the host arrays); an emulated rank (args.emulate = (rank, world), one GPU) checks its strip."""
     ntr = args.tracers
+    em = getattr(args, "emulate", None)
+    if em:
+        rank, world = em
     nx, ny, nl = global_dims(args, world)
     R0, R1 = partition.strip_rows(ny, world, rank) if world > 1 else (0, ny)
-    run_check_pass(args, e, step, m, ntr)
+    if check_pass is not None:
+        check_pass()
+    else:
+        run_check_pass(args, e, step, m, ntr)
+    if fetch is None:
+        fetch = lambda name, out: e.download(name, out=out)
     # strips of about 80k nodes (a few seconds of oracle work each), at least one per worker
     rows = R1 - R0
     nstrip = max(min(rows, ctx.nworkers), min(rows, -(-(rows * nx) // 80000)))
@@ -479,7 +550,8 @@ def verify_parallel(args, ctx, e, step, m, world, rank):
     strips = [(cuts[s_], cuts[s_ + 1]) for s_ in range(nstrip) if cuts[s_ + 1] > cuts[s_]]
     # the outputs reach the workers as memory-mapped files in /dev/shm when it has room for every
     # rank's (no copy), else as the strips' slices sent with the jobs
-    need = sum(8 * max(e.size(name), 1) for name, _ in OUTPUTS)
+    sizes = {name: ntr * e.size(name) // e.ntr for name, _ in OUTPUTS}
+    need = sum(8 * max(sizes[name], 1) for name, _ in OUTPUTS)
     shm = "/dev/shm"
     try:
         st_ = os.statvfs(shm)
@@ -492,18 +564,22 @@ def verify_parallel(args, ctx, e, step, m, world, rank):
         if use_files:
             import tempfile
             for name, _ in OUTPUTS:
-                n = e.size(name)
+                n = sizes[name]
                 fd, path = tempfile.mkstemp(prefix=f"f2a_check_{os.getpid()}_{name}_", dir=shm)
                 os.close(fd)
                 paths.append(path)
                 buf = np.memmap(path, dtype=np.float64, mode="w+", shape=(max(n, 1),))
-                e.download(name, out=buf)
+                fetch(name, buf)
                 buf.flush()
                 del buf
                 files[name] = (path, (ntr, n // ntr))
             srcs = [("files", files)] * len(strips)
         else:
-            host = {name: e.download(name).reshape(ntr, -1) for name, _ in OUTPUTS}
+            host = {}
+            for name, _ in OUTPUTS:
+                host[name] = np.empty(max(sizes[name], 1))
+                fetch(name, host[name])
+                host[name] = host[name][: sizes[name]].reshape(ntr, -1)
             srcs = []
             for a, b in strips:
                 e0, e1 = strip_edge_range(nx, ny, R0, R1, a, b)
@@ -575,6 +651,80 @@ def verify(args, ctx, e, step, m, fields, world, lists, want=None):
                         "oracle/fct_ale_oracle.c full pass on the same mesh (per tracer)")}
 
 
+# ----------------------------------------------------------------------------- PCIe / halo helpers
+
+def pcie_probe(nbytes=1 << 30, reps=5):
+    """What this box's PCIe link moves between page-locked host memory and HBM, through the
+    library's own transfer entries: H2D (transfer_var_, synchronous), D2H (fesom2_download_ into a
+    pinned array) and both directions at once (transfer_var_async_ and fesom2_transfer_back_async_
+    on two streams), 1 GiB each, best of ``reps``."""
+    n = nbytes // 8
+    bufs, hps, hs = [], [], []
+    try:
+        for _ in range(2):
+            a, hp = abi.pinned(n)
+            a[:] = 1.0
+            h = abi.Handle("pcie")
+            abi.check(abi.alloc_var(h, a), "alloc_var_(pcie)")
+            bufs.append(a)
+            hps.append(hp)
+            hs.append(h)
+        s1, s2 = abi.Stream(), abi.Stream()
+
+        def best(fn):
+            t = []
+            for _ in range(reps):
+                abi.device_sync()
+                t0 = time.perf_counter()
+                fn()
+                abi.device_sync()
+                t.append(time.perf_counter() - t0)
+            return min(t)
+
+        st = C.c_int(0)
+        h2d = best(lambda: abi.dll().transfer_var_(hs[0].ref, abi.arr(bufs[0])))
+        d2h = best(lambda: abi.dll().fesom2_download_(hs[0].ref, abi.arr(bufs[0]), C.byref(st)))
+
+        def duplex():
+            abi.transfer_var_async(hs[0], bufs[0], s1)
+            abi.transfer_back_async(hs[1], bufs[1], s2)
+        dup = best(duplex)
+        for h in hs:
+            abi.dll().fesom2_free_(h.ref)
+        for s_ in (s1, s2):
+            abi.dll().fesom2_free_stream_(s_.ref)
+        return {"h2d_GBps": round(nbytes / h2d / 1e9, 2), "d2h_GBps": round(nbytes / d2h / 1e9, 2),
+                "duplex_GBps_each_way": round(nbytes / dup / 1e9, 2), "bytes": nbytes,
+                "method": "1 GiB page-locked (allocate_pinned_doubles_) <-> one handle: transfer_var_ (H2D), "
+                          "fesom2_download_ (D2H), transfer_var_async_ + fesom2_transfer_back_async_ on two "
+                          f"streams at once (duplex); best of {reps}"}
+    finally:
+        for hp in hps:
+            abi.free_pinned(hp)
+
+
+def oracle_halo_plus_minus(nx, ny, nl, full_depth, vlimit, world, rank):
+    """plus/minus of the halo rows of rank's strip of the world-way y-strip split of the nx x ny
+    structured mesh (rows y0 - 1 and y1) from the oracle on those rows alone (each a one-row strip
+    with its own one-ring halo: exact), (H, L) in the local halo order -- what the exchange would
+    deliver; the emulated-rank leg's check uses it (tests/test_bench.py checks it against the
+    single-domain pass)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    y0, y1 = partition.strip_rows(ny, world, rank)
+    rows = ([y0 - 1] if y0 > 0 else []) + ([y1] if y1 < ny else [])
+    L = nl - 1
+    plus, minus = np.zeros((len(rows) * nx, L)), np.zeros((len(rows) * nx, L))
+    for k, j in enumerate(rows):
+        mh, _ = partition.strip_local_mesh(nx, ny, nl, j, j + 1, full_depth=full_depth)
+        st, p1 = O.pre_comm(mh, synth.make_fields(mh), vlimit=vlimit)
+        if st != 5:
+            raise RuntimeError(f"oracle pre_comm (halo row {j}) stopped at alg_state {st}")
+        plus[k * nx:(k + 1) * nx] = p1["plus"][: nx * L].reshape(nx, L)
+        minus[k * nx:(k + 1) * nx] = p1["minus"][: nx * L].reshape(nx, L)
+    return plus, minus
+
+
 # ----------------------------------------------------------------------------- one leg
 
 class Ctx:
@@ -585,6 +735,7 @@ class Ctx:
     pool = None
     nworkers = 0
     watchdog = None
+    pcie = None  # pcie_probe(), once per run (the transfer legs)
 
     def barrier(self):
         if self.dist is not None:
@@ -604,6 +755,9 @@ class Ctx:
 def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     """Build, warm up, time K steps, break the kernels down, check.  Returns the leg's record."""
     rank, world, dist = ctx.rank, ctx.world, ctx.dist
+    if args.transfers and ctx.pcie is None:
+        ctx.pcie = pcie_probe()
+        log(f"pcie probe: {ctx.pcie}")
     t_setup = time.perf_counter()
     m, lists = build_local(args, rank, world)
     if args.tracers > 1 and args.path in ("stepwise", "reference", "reference-plain"):
@@ -611,35 +765,51 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     fields = synth.make_tracer_fields(m, args.tracers)
     f = fields[0]
     pinned = []
-    if args.transfers:
-        if world > 1 or args.tracers > 1 or args.check:
-            raise SystemExit("--transfers: 1 GPU, 1 tracer, no --check (outputs land in the input host arrays)")
-        args.path = "reference"
-        pf = {}
-        zeros = np.zeros((m.N + m.H) * m.L)
-        for k, v in list(f.items()) + [("plus", zeros), ("minus", zeros)]:
-            # page-locked host arrays, as FESOM2 would use allocate_pinned_doubles_
-            hp, st = C.c_void_p(), C.c_int(0)
-            abi.dll().allocate_pinned_doubles_(C.byref(hp), C.byref(C.c_int(v.size)), C.byref(st))
-            a = np.ctypeslib.as_array((C.c_double * v.size).from_address(hp.value))
-            a[:] = v
-            pf[k] = a
-            pinned.append(hp)
-        fields = [pf]
-        f = pf
-    abi.set_resident(not args.transfers)
+    mode = args.transfers  # None (device resident), "reference" or "producer" (host transfers in the step)
+    # the fields a transfer step moves per tracer: the producer's (fct_ale_muscl_LH's) ttf, LO,
+    # fct_adf_v, fct_adf_h and the host-accumulated del_ttf_advvert / del_ttf_advhoriz; with the
+    # reference semantics also fct_plus/fct_minus (the host's exchange_nod round trip)
+    streamed = ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")
+    if mode:
+        if world > 1 or getattr(args, "emulate", None) or args.mesh != "structured" or args.fct_iter > 1:
+            raise SystemExit("--transfers: 1 GPU, structured mesh, one FCT iteration")
+        if mode == "reference" and args.tracers != 1:
+            raise SystemExit("--transfers reference: 1 tracer (the reference's entries take one)")
+        if mode == "producer" and args.tracers != 2:
+            raise SystemExit("--transfers producer: 2 tracers, one stream each")
+        args.path = "reference" if mode == "reference" else "split"
+        if mode == "reference":
+            streamed += ("plus", "minus")
+        pfs = []
+        for fk in fields:
+            pf = dict(fk)
+            for k in streamed:
+                v = fk[k] if k in fk else np.zeros((m.N + m.H) * m.L)
+                a, hp = abi.pinned(v.size)  # page-locked, as FESOM2 would use allocate_pinned_doubles_
+                a[:] = v
+                pf[k] = a
+                pinned.append(hp)
+            pfs.append(pf)
+        fields = pfs
+        f = fields[0]
+    abi.set_resident(mode != "reference")
     abi.set_path({"stepwise": "stepwise", "reference": "reference"}.get(args.path, "fused"))
     dm = engine.DeviceMesh(m)
     dm.prepare()
-    mi = dm.info(batched=args.tracers > 1)
+    mi = dm.info(batched=args.tracers > 1 and mode != "producer")
     mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
-    order = dm.pass_order(args.tracers)  # the Infinity-Cache pass order the entries use
-    if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or args.transfers):
+    order = dm.pass_order(args.tracers if mode != "producer" else 1)  # the Infinity-Cache pass order
+    if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or mode):
         raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
-    e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
-        engine.FctAleBatch(dm, fields, vlimit=args.vlimit)
+    if mode == "producer":  # one single-tracer engine (and stream) per tracer
+        engines = [engine.FctAle(dm, fk, copy=False, vlimit=args.vlimit) for fk in fields]
+        e = engines[0]
+    else:
+        e = engine.FctAle(dm, f, copy=False, vlimit=args.vlimit) if args.tracers == 1 else \
+            engine.FctAleBatch(dm, fields, vlimit=args.vlimit)
+        engines = [e]
     parallel_check = (args.check and ctx.pool is not None and args.mesh == "structured" and not args.permuted
-                      and args.fct_iter == 1 and not args.transfers)
+                      and args.fct_iter == 1)
     cpu_leg = headline and rank == 0 and world == 1 and not args.no_cpu_baseline
     if parallel_check and not cpu_leg:
         # the check regenerates its pristine inputs: no second host copy of the fields
@@ -678,10 +848,12 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
 
     def step_transfers():
         """FESOM2 with the reference's transfer semantics: the producer uploads ttf/adf_v/adf_h
-        (src/fesom2-accelerate.cu:269-270), each phase moves its own fields, the host waits after
-        phase 1 (where exchange_nod would run) and at the end."""
-        for k in ("ttf", "adf_v", "adf_h"):
-            abi.dll().transfer_var_async_(e.h[k].ref, abi.arr(e.host[k]), e.stream.ref, C.byref(C.c_bool(True)))
+        (src/fesom2-accelerate.cu:269-270) and the host's del_ttf_advvert/advhoriz, each phase moves
+        its own fields (pre_comm: LO up, plus/minus down, :268, :337-339; inter_comm: adf_v down,
+        :354-355; post_comm: plus/minus up, adf_h down, :364-365, :377-378; c-step: del_ttf down),
+        the host waits after phase 1 (where exchange_nod would run) and at the end."""
+        for k in ("ttf", "adf_v", "adf_h", "del_v", "del_h"):
+            abi.transfer_var_async(e.h[k], e.host[k], e.stream, k in ("ttf", "adf_v", "adf_h"))
         if e.pre_comm() != 6:
             raise RuntimeError(f"pre_comm: {abi.last_error()}")
         e.sync()
@@ -689,9 +861,29 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
             raise RuntimeError(f"phase 2: {abi.last_error()}")
         e.sync()
 
+    def step_producer():
+        """Device-resident split pass of two tracers, each on its own stream, with the host's uploads
+        of the producer's fields and the download of del_ttf inside the step: tracer 1's uploads
+        overlap tracer 0's pass and tracer 0's downloads; the host waits for both at the end."""
+        for ek in engines:
+            for k in streamed:
+                abi.transfer_var_async(ek.h[k], ek.host[k], ek.stream, k in ("ttf", "adf_v", "adf_h"))
+            s1 = ek.pre_comm_v()
+            if s1 != 7:
+                raise RuntimeError(f"pre_comm_v alg_state {s1}: {abi.last_error()}")
+            s2 = ek.post_comm_h()
+            if s2 != 9:
+                raise RuntimeError(f"post_comm_h alg_state {s2}: {abi.last_error()}")
+            for k in ("del_v", "del_h"):
+                abi.transfer_back_async(ek.h[k], ek.host[k], ek.stream)
+        for ek in engines:
+            ek.sync()
+
     def step():
-        if args.transfers:
+        if mode == "reference":
             return step_transfers()
+        if mode == "producer":
+            return step_producer()
         if args.fct_iter > 1:  # iter_yn: K-1 rounds of phase 1 + iterative phase 2, then the final pass
             s_it = e.iterated_pass(args.fct_iter, final="split" if args.path == "split" else "fused")
             if s_it != 9:
@@ -740,7 +932,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
 
     graph = None
     if args.graph:
-        if args.transfers or (world > 1 and args.exchange == "host"):
+        if mode or (world > 1 and args.exchange == "host"):
             raise SystemExit("--graph needs device-resident steps without host exchange")
         abi.device_sync()
         with abi.Graph.capture(stream) as graph:
@@ -752,7 +944,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         abi.device_sync()
 
     # ---- timed region: exactly K steps, barrier + device sync on both sides
-    timing = not args.graph and args.kernel_timing != "none"
+    timing = not args.graph and args.kernel_timing != "none" and not mode  # transfer legs: wall time only
     # the split pass's dominant kernel is p1v (an iterated FCT call is dominated by its iteration kernels)
     timed_only = args.kernel_timing == "dominant" and args.path == "split" and args.fct_iter == 1 and not args.graph
     abi.kernel_timing_only("fct_ale_p1v" if timed_only else None)
@@ -832,7 +1024,8 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
             continue
         if tr.get("workload") == args.config and tr.get("tracers", 1) == args.tracers and \
                 args.mesh == "structured" and not args.parity_levels and args.vlimit == 1 and \
-                args.fct_iter == 1 and args.scaling == "weak" and dom in tr.get("bytes_per_launch", {}):
+                args.fct_iter == 1 and (args.scaling == "weak" or (world == 1 and not getattr(args, "emulate", None))) \
+                and not args.transfers and dom in tr.get("bytes_per_launch", {}):
             traffic = tr["bytes_per_launch"][dom]
             break
     roof = None
@@ -852,11 +1045,15 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         if traffic:
             roof["traffic_over_alg"] = round(traffic / kb[dom], 3)
         if ceiling:  # context: what this GPU streams (copy) and streams in p1v's pattern, same run
-            roof["stream_ceiling"] = dict(ceiling, frac_of_copy=round(achieved / ceiling["copy_GBps"], 4),
-                                          tool="tools/stream_probe.hip")
-            if dom == "fct_ale_p1v" and args.tracers == 1:
-                roof["stream_ceiling"]["frac_of_p1v_pattern"] = round(achieved / ceiling["p1v_pattern_GBps"], 4)
-    pass_gbs = kb["survey_pass"] / (ms_step * 1e-3) / 1e9
+            roof["stream_ceiling"] = dict(ceiling, tool="tools/stream_probe.hip")
+            roof["frac_of_copy"] = round(achieved / ceiling["copy_GBps"], 4)
+            # p1v's own stream pattern (no gathers): one tracer's, or the batch's (tracer-fastest tiles
+            # of the plan's block size) for a batched call
+            pat = ceiling.get("p1v_pattern_GBps") if args.tracers == 1 else \
+                ceiling.get("batch_GBps", {}).get(str(args.tracers))
+            if dom == "fct_ale_p1v" and pat:
+                roof["frac_of_p1v_pattern"] = round(achieved / pat, 4)
+                roof["p1v_pattern_GBps"] = pat
 
     # ---- CPU baseline (rank 0, N = 1, headline only)
     cpu = None
@@ -870,7 +1067,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         cpu = {"value": round(s["cn"] / best, 1), "unit": "cell-updates/s", "cores": 1, "kind": "port",
                "sample": f"oracle/fct_ale_oracle.c full pass a1..c (a1..b2 bit-identical to reference.cpp), "
                          f"single thread, same {args.config} mesh, best of {reps} passes ({best:.2f} s/pass)",
-               "all_cores": cpu_all, "host": host_info()}
+               "per_gpu_share": cpu_all, "host": host_info()}
         t_ref = O.time_ref_pre_comm(m, f)
         if t_ref is not None:
             cpu["reference_phase1"] = {
@@ -880,8 +1077,56 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
                           f"best of 2 ({t_ref:.2f} s per phase 1)"}
 
     check = None
-    if args.check and not args.transfers:  # --transfers: outputs land in the input host arrays
-        if parallel_check and oracle_want is None:
+    em = getattr(args, "emulate", None)
+    if args.check:
+        if mode:
+            # the transfer legs: pristine inputs into the host arrays the step uploads, one step, then
+            # the outputs where the host gets them (the reference semantics: every output comes back
+            # to the host arrays; producer mode: del_ttf on the host, the rest on the device)
+            host_out = set(streamed) if mode == "reference" else {"del_v", "del_h"}
+
+            def transfer_check_pass():
+                for k, ek in enumerate(engines):
+                    for name in streamed:
+                        if name in ("plus", "minus"):
+                            ek.host[name][:] = 0.0
+                        else:
+                            ek.host[name][:] = synth.make_field(m, name, seed=43 + k)
+                step()
+                abi.device_sync()
+
+            def transfer_fetch(name, out):
+                n = e.size(name)
+                for k, ek in enumerate(engines):
+                    out[k * n:(k + 1) * n] = ek.host[name][:n] if name in host_out else ek.download(name)
+
+            check = verify_parallel(args, ctx, e, step, m, world, rank, check_pass=transfer_check_pass,
+                                    fetch=transfer_fetch)
+        elif em:
+            # one strip of the strong split without an exchange in its timed steps: the check pass
+            # takes the halo plus/minus the exchange would deliver from the oracle (halo rows only)
+            hp_, hm_ = oracle_halo_plus_minus(*global_dims(args, em[1]), not args.parity_levels, args.vlimit,
+                                              em[1], em[0])
+
+            def emulated_check_pass():
+                for name in ("adf_v", "adf_h", "del_v", "del_h"):
+                    e.upload(name, pristine(m, name, 1))
+                s1 = e.pre_comm_v()
+                if s1 != 7:
+                    raise RuntimeError(f"pre_comm_v alg_state {s1}: {abi.last_error()}")
+                e.sync()
+                for name, halo_vals in (("plus", hp_), ("minus", hm_)):
+                    a = e.download(name).reshape(-1, m.L)
+                    a[m.N:m.N + m.H] = halo_vals
+                    e.upload(name, a.reshape(-1))
+                s2 = e.post_comm_h()
+                if s2 != 9:
+                    raise RuntimeError(f"post_comm_h alg_state {s2}: {abi.last_error()}")
+                abi.device_sync()
+
+            check = verify_parallel(args, ctx, e, step, m, world, rank, check_pass=emulated_check_pass)
+            check["halo"] = "plus/minus of the two halo rows from the oracle (what the exchange delivers)"
+        elif parallel_check and oracle_want is None:
             check = verify_parallel(args, ctx, e, step, m, world, rank)  # a replay when --graph
         else:
             check = verify(args, ctx, e, step, m, fields, world, lists, oracle_want)
@@ -890,9 +1135,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         graph.free()
 
     rec = {"value": round(value, 1), "ms_per_step": round(ms_step, 4), "roofline": roof,
-           "pass_roofline": {"alg_bytes": kb["survey_pass"], "GBps": round(pass_gbs, 1),
-                             "frac": round(pass_gbs / (HBM_PEAK / 1e9), 4),
-                             "note": "SURVEY.md 8(d) B_pass = 32 Cn + ntracers (120 Cn + 24 Ce) over the whole pass"},
+           "pass_roofline": pass_roofline(kb["survey_pass"], ms_step, ceiling),
            "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
            "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s,
            "pass_order": order}
@@ -913,6 +1156,38 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         ci = halo.info()
         rec["rccl_nranks"] = ci["nranks"]  # ncclCommCount of the communicator the exchange ran on
         rec["rccl"] = ci
+    if mode:
+        # PCIe traffic of one step (both tracers in producer mode) and its rate against the same
+        # run's probe of the link (ctx.pcie, measured once before the first transfer leg)
+        NT, L, nl, E = m.N + m.H, m.L, m.nl, m.E
+        per = {"ttf": NT * L, "LO": NT * L, "del_v": NT * L, "del_h": NT * L, "plus": NT * L, "minus": NT * L,
+               "adf_v": NT * nl, "adf_h": E * L}
+        if mode == "reference":
+            up = [*streamed]                                          # producer's + LO + plus/minus (post_comm)
+            down = ["plus", "minus", "adf_v", "adf_h", "del_v", "del_h"]
+        else:
+            up, down = list(streamed), ["del_v", "del_h"]
+        h2d = 8 * len(engines) * sum(per[k] for k in up)
+        d2h = 8 * len(engines) * sum(per[k] for k in down)
+        sec = ms_step * 1e-3
+        pc = ctx.pcie or {}
+        rec["transfers"] = {
+            "mode": {"reference": "reference transfer semantics: pre_comm -> inter_comm -> post_comm -> c_acc_, "
+                                  "every phase's own H2D/D2H (src/fesom2-accelerate.cu:268, :337-339, :354-355, "
+                                  ":364-365, :377-378), fast mode, the producer's uploads inside the step",
+                     "producer": "device-resident split pass, per tracer on its own stream: the producer's "
+                                 "uploads (ttf, LO, fct_adf_v, fct_adf_h, del_ttf in) and del_ttf out inside the "
+                                 "step, two tracers overlapped"}[mode],
+            "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+            "h2d_GBps": round(h2d / sec / 1e9, 2), "d2h_GBps": round(d2h / sec / 1e9, 2),
+            "h2d_frac_of_probe": round(h2d / sec / 1e9 / pc["h2d_GBps"], 3) if pc.get("h2d_GBps") else None,
+            "d2h_frac_of_probe": round(d2h / sec / 1e9 / pc["d2h_GBps"], 3) if pc.get("d2h_GBps") else None,
+            # both directions at the probe's duplex rate at once: the step's floor on this link
+            "pcie_floor_ms": round(1e3 * max(h2d, d2h) / (pc["duplex_GBps_each_way"] * 1e9), 2)
+            if pc.get("duplex_GBps_each_way") else None,
+            "probe": pc}
+    for ek in engines[1:]:
+        ek.free()
     e.free()
     dm.free()
     for hp in pinned:
@@ -941,7 +1216,18 @@ def extra_legs(args, world):
                 ("config1_127kx47_6tracers", dict(config="127k x 47", tracers=6, scaling="weak",
                                                   steps=max(args.steps, 80), warmup=max(args.warmup, 10))),
                 ("config3_1p2Mx80_6tracers", dict(config="1.2M x 80", tracers=6, scaling="weak")),
-                strong]
+                strong,
+                # BASELINE configs[4]'s N = 8 point, one rank's share: an interior strip (two neighbours)
+                # of the 8-way strong split, 3200 x 375 rows = 1.2M nodes, on this GPU
+                (strong[0].replace("config4_strong_", "config4_strong_rank3of8_"),
+                 dict(strong[1], emulate=(3, 8))),
+                # SURVEY.md 8(d)'s transfer-inclusive rates at 1.2M x 80 (PCIe inside the step)
+                ("config2_transfers_reference", dict(config="1.2M x 80", tracers=1, scaling="weak",
+                                                     transfers="reference", steps=min(args.steps, 10),
+                                                     warmup=min(args.warmup, 2))),
+                ("config2_transfers_producer_2tracers", dict(config="1.2M x 80", tracers=2, scaling="weak",
+                                                             transfers="producer", steps=min(args.steps, 10),
+                                                             warmup=min(args.warmup, 2)))]
     return [strong]
 
 
@@ -955,9 +1241,13 @@ def compact(rec, args, world):
            "roofline": rec["roofline"], "pass_roofline": rec["pass_roofline"],
            "kernels_ms": {k: v["avg_ms"] for k, v in rec["kernels"].items()}, "check": rec["check"],
            "setup_s": rec["setup_s"], "pass_order": rec["pass_order"]}
-    for k in ("ranks", "rccl_nranks"):
+    for k in ("ranks", "rccl_nranks", "transfers"):
         if k in rec:
             out[k] = rec[k]
+    if getattr(args, "emulate", None):
+        out["emulated_rank"] = {"rank": args.emulate[0], "of": args.emulate[1],
+                                "note": "one strip of the strong split on this GPU (halo from global ids), no "
+                                        "exchange in the timed steps: the per-rank compute of that N-GPU point"}
     return out
 
 
@@ -990,10 +1280,16 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="capture one step into a hipGraph after the warmup and time K replays (no host-side "
                          "work per step; per-kernel timing and roofline are then not available)")
-    ap.add_argument("--transfers", action="store_true",
-                    help="reference transfer semantics (fesom2_set_resident_(0)): pinned host arrays, the producer's "
-                         "H2D of ttf/adf_v/adf_h and every phase's own H2D/D2H inside the timed step, reference entry "
-                         "sequence; a PCIe-inclusive rate for DESIGN.md, not the benchmark value (1 GPU, 1 tracer)")
+    ap.add_argument("--transfers", nargs="?", const="reference", default=None, choices=["reference", "producer"],
+                    help="PCIe inside the timed step, pinned host arrays (1 GPU): 'reference' (the default of the bare "
+                         "flag) the reference transfer semantics (fesom2_set_resident_(0), the reference entry sequence, "
+                         "every phase's own H2D/D2H, the producer's uploads; 1 tracer); 'producer' the device-resident "
+                         "split pass with only the producer's uploads and del_ttf's download in the step, two tracers "
+                         "on two streams (--tracers 2).  A PCIe-inclusive rate, not the benchmark value")
+    ap.add_argument("--emulate-rank", default=None,
+                    help="R/N: time rank R's strip of an N-way --scaling strong split on this one GPU (halo from "
+                         "global ids, no exchange in the timed steps; the check takes the halo plus/minus from the "
+                         "oracle): the per-rank compute of the N-GPU point")
     ap.add_argument("--vlimit", type=int, default=1, choices=[1, 2, 3],
                     help="vertical limiter of a3 (docs/refactoring.md:113-148; reference.cpp has 1 only)")
     ap.add_argument("--fct-iter", type=int, default=1,
@@ -1031,9 +1327,16 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="measured HBM bytes per launch (rocprofv3 PMC, see profiles/)")
     args = ap.parse_args()
+    if args.emulate_rank:
+        r_, n_ = (int(v) for v in args.emulate_rank.split("/"))
+        if not (0 <= r_ < n_ and n_ > 1):
+            raise SystemExit("--emulate-rank R/N with 0 <= R < N, N > 1")
+        args.emulate = (r_, n_)
+    args.emulate_rank = None
     default_workload = args.config is None and args.scaling == "weak" and args.tracers == 1 and \
         args.mesh == "structured" and not (args.permuted or args.parity_levels or args.graph or args.transfers) and \
-        args.vlimit == 1 and args.fct_iter == 1 and args.path == "split" and args.exchange == "rccl"
+        args.vlimit == 1 and args.fct_iter == 1 and args.path == "split" and args.exchange == "rccl" and \
+        not getattr(args, "emulate", None)
     if args.config is None:
         args.config = "1.2M x 80" if args.scaling == "weak" else "9.6M x 80"
     args.leg = "headline"
@@ -1053,13 +1356,19 @@ def main():
         ctx.pool, ctx.nworkers = make_pool(world)
     cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_all = cpu_all_cores(args, ctx.pool, ctx.nworkers)
-        log(f"cpu all cores: {cpu_all}")
+        cpu_all = cpu_per_gpu_share(args, ctx.pool, ctx.nworkers)
+        log(f"cpu per-GPU share: {cpu_all}")
 
-    ceiling = None
+    # the stream probes (own processes, before this one touches the GPU): the headline's size (with
+    # the 6-tracer batched pattern when the extra legs run) and the small partition's
+    ceilings = {}
+    extras_on = (default_workload and args.extras == "auto") or args.extras == "on"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ceiling = stream_ceiling(args)  # own process, before this one touches the GPU
-        log(f"stream ceiling: {ceiling}")
+        ceilings[args.config] = stream_ceiling(args.config, 6 if extras_on else args.tracers)
+        if extras_on and args.config != "127k x 47":
+            ceilings["127k x 47"] = stream_ceiling("127k x 47")
+        log(f"stream ceilings: {ceilings}")
+    ceiling = ceilings.get(args.config)
 
     abi.dll()  # engine first: one HIP runtime for the process
     abi.set_mpi_rank(local_rank, world)  # reference set_mpi_rank_: device = rank % ndev
@@ -1118,7 +1427,7 @@ def main():
     exact = out.get("check") is None or out["check"]["exact"]
 
     # ---- further BASELINE configs in the same run
-    if (default_workload and args.extras == "auto") or args.extras == "on":
+    if extras_on:
         out["extra"] = {}
 
         def partial(stage):  # watchdog on rank 0: the headline is measured, print what there is
@@ -1134,8 +1443,11 @@ def main():
             la.traffic = os.path.join(ROOT, "profiles", "none.json")  # the per-config traffic files below
             ctx.watchdog.arm(f"extra leg {name}", args.leg_timeout)
             t0 = time.perf_counter()
+            # the 9.6M x 80 strip columns stream like 1.2M x 80's (same column shape, both far past the
+            # caches): that probe is their ceiling
+            lc = ceilings.get(la.config) or (ceilings.get("1.2M x 80") if la.config == "9.6M x 80" else None)
             try:
-                rec = run_leg(la, ctx)
+                rec = run_leg(la, ctx, ceiling=lc)
             except Exception as ex:  # an extra leg must not cost the measured headline its line
                 ctx.watchdog.disarm()
                 log(f"rank {rank}: extra leg {name} failed: {type(ex).__name__}: {ex}")

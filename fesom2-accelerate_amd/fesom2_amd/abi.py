@@ -218,6 +218,33 @@ class _Capture:
         return False
 
 
+def pinned(n):
+    """A page-locked host array of n doubles (allocate_pinned_doubles_, as a FESOM2 host would
+    allocate its transfer buffers) and its pointer (free with free_pinned)."""
+    hp, st = C.c_void_p(), C.c_int(0)
+    dll().allocate_pinned_doubles_(C.byref(hp), C.byref(C.c_int(int(max(n, 1)))), C.byref(st))
+    if st.value or not hp.value:
+        raise HipError(f"allocate_pinned_doubles_({n}) fell back to pageable memory: {last_error()}")
+    import numpy as np
+    return np.ctypeslib.as_array((C.c_double * int(max(n, 1))).from_address(hp.value))[:n], hp
+
+
+def free_pinned(hp):
+    dll().fesom2_free_pinned_(C.byref(hp))
+
+
+def transfer_var_async(h, a, stream, record_event=False):
+    """transfer_var_async_: rebind h's host array to ``a`` and enqueue its H2D on ``stream``."""
+    dll().transfer_var_async_(h.ref, arr(a), stream.ref, bp(record_event))
+
+
+def transfer_back_async(h, a, stream):
+    """fesom2_transfer_back_async_: rebind h's host array to ``a`` and enqueue its D2H on ``stream``."""
+    st = C.c_int(0)
+    dll().fesom2_transfer_back_async_(h.ref, arr(a), stream.ref, C.byref(st))
+    check(st, "fesom2_transfer_back_async_")
+
+
 def set_resident(on):
     dll().fesom2_set_resident_(ip(1 if on else 0))
 

@@ -59,9 +59,53 @@ def test_split_pass_bytes_close_to_survey_minimum(stats):
 
 def test_stream_ceiling_without_a_gpu_is_none():
     """On a machine without a GPU the probe fails and the bench reports no ceiling (no exception)."""
-    class A:
-        config = "8k x 20"
-    assert bench.stream_ceiling(A()) is None
+    assert bench.stream_ceiling("8k x 20") is None
+    assert bench.stream_ceiling("8k x 20", 6) is None
+
+
+def test_pass_roofline_against_the_copy_rate():
+    """pass_roofline: SURVEY.md 8(d)'s pass bytes per second against 8 TB/s (frac) and against the
+    same run's flat-copy rate (frac_of_copy): the cross-round figure of the driver line."""
+    r = bench.pass_roofline(21.5e9, 4.0, {"copy_GBps": 6250.0, "p1v_pattern_GBps": 5400.0})
+    assert r["GBps"] == pytest.approx(5375.0) and r["frac"] == pytest.approx(5375.0 / 8000.0, abs=1e-4)
+    assert r["copy_GBps"] == 6250.0 and r["frac_of_copy"] == pytest.approx(0.86, abs=1e-4)
+    assert "frac_of_copy" not in bench.pass_roofline(21.5e9, 4.0, None)
+
+
+@pytest.mark.parametrize("world,rank,full", [(4, 1, True), (4, 3, False), (3, 0, False)])
+def test_emulated_rank_check_halo_is_the_single_domain_pass(world, rank, full):
+    """The emulated-rank leg (one strip of the strong split on one GPU, no exchange) checks its pass
+    with the halo plus/minus bench.oracle_halo_plus_minus computes from the halo rows alone: with
+    them, phase 2 on the strip equals the single-domain pass on every owned cell and local edge."""
+    import oracle as O
+    nx, ny, nl = 20, 16, 11
+    g = synth.make_mesh(nx, ny, nl, full_depth=full)
+    want = O.full_pass(g, synth.make_fields(g))
+    y0, y1 = partition.strip_rows(ny, world, rank)
+    m, _ = partition.strip_local_mesh(nx, ny, nl, y0, y1, full_depth=full)
+    f = synth.make_fields(m)
+    st, p1 = O.pre_comm(m, f)
+    assert st == 5
+    hp, hm = bench.oracle_halo_plus_minus(nx, ny, nl, full, 1, world, rank)
+    L = m.L
+    assert hp.shape == (m.H, L)
+    plus, minus = p1["plus"].reshape(-1, L).copy(), p1["minus"].reshape(-1, L).copy()
+    gid = m.node_gid
+    wet = np.arange(L)[None, :] < (m.nlev_nod[m.N:, None].astype(np.int64) - 1)
+    assert np.array_equal(hp[wet], want["plus"].reshape(-1, L)[gid[m.N:]][wet])
+    assert np.array_equal(hm[wet], want["minus"].reshape(-1, L)[gid[m.N:]][wet])
+    plus[m.N:], minus[m.N:] = hp, hm
+    r = O.post_comm(m, f, plus.reshape(-1), minus.reshape(-1))
+    for name, w in (("del_v", L), ("del_h", L), ("adf_v", nl)):
+        assert np.array_equal(r[name].reshape(-1, w)[: m.N], want[name].reshape(-1, w)[gid[: m.N]]), name
+    assert np.array_equal(r["adf_h"].reshape(-1, L), want["adf_h"].reshape(-1, L)[m.edge_gid])
+
+
+def test_cpu_baseline_host_counts_physical_cores():
+    """The CPU baseline states what it represents: the host's physical cores (for the per-GPU share
+    and the full-host estimate) beside nproc."""
+    h = bench.host_info()
+    assert h["nproc"] >= 1 and (h["physical_cores"] is None or 1 <= h["physical_cores"] <= h["nproc"])
 
 
 def test_bench_help_runs_on_cpu():

@@ -9,8 +9,9 @@
 //          stride-nl arrays at nl = L+1 (8-byte aligned 16-B loads), adf_h as three columns per node
 // Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe tools/stream_probe.hip (build() does)
 // Run:   ./stream_probe [nodes=1200000] [L=80] [--json|--text] [tracers]  (--json: one line with the copy
-//        and the G = 8 column-pattern rates, which bench.py reports beside the roofline; tracers > 1
-//        adds the batched pattern, one line per block shape and tile order)
+//        and the G = 8 column-pattern rates -- odd L: p1v's slot shape at the ABI stride --, which
+//        bench.py reports beside the roofline; tracers > 1 adds the batched pattern, one line per
+//        block shape and tile order, before it)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -230,7 +231,7 @@ int main(int argc, char **argv)
             hipLaunchKernelGGL(k_flat, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, 0, a, np);
         });
     for (int G : {4, 8, 16, 24}) {
-        if (json && G != 8) continue;
+        if (json && (G != 8 || L % 2 == 1)) continue;
         char nm[64];
         snprintf(nm, sizeof nm, "cols G=%d 11R+4W", G);
         const int thr = ((G * (L / 2) + 63) / 64) * 64;
@@ -239,15 +240,17 @@ int main(int argc, char **argv)
         });
         if (G == 8) cols_tbs = r;
     }
-    if (!json && L % 2 == 1) {  // odd L: p1v's slot shape, ABI stride vs padded vs parity-aware pairs
+    if (L % 2 == 1) {  // odd L: p1v's slot shape, ABI stride vs padded vs parity-aware pairs
         const int G = 8, S = (L + 1) / 2, thr = ((G * S + 63) / 64) * 64;
         for (int mode = 0; mode < 3; mode++) {
+            if (json && mode != 0) continue;
             const char *nm[3] = {"odd cols stride L", "odd cols stride L+1", "odd cols aligned pairs"};
             const int stride = mode == 1 ? L + 1 : L;
-            timeit(nm[mode], bytes_p1, [&] {
+            const double r = timeit(nm[mode], bytes_p1, [&] {
                 hipLaunchKernelGGL(k_cols_odd, dim3((unsigned)((nodes + G - 1) / G)), dim3(thr), 0, 0, a, (int)nodes, L,
                                    G, stride, mode == 2 ? 1 : 0);
             });
+            if (mode == 0) cols_tbs = r;  // --json: p1v's own shape at odd L (the ABI stride)
         }
     }
     if (!json) {  // the same without the XCD-contiguous tile ranges (block b -> tile b)
