@@ -1134,8 +1134,15 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     if graph is not None:
         graph.free()
 
+    # the whole pass's figures also inside `roofline` (the driver's parsed record keeps that object
+    # whole; pass_roofline stays beside it): frac of 8 TB/s and of this run's copy rate
+    pr = pass_roofline(kb["survey_pass"], ms_step, ceiling)
+    if roof is not None:
+        roof["pass_frac"] = pr["frac"]
+        if "frac_of_copy" in pr:
+            roof["pass_frac_of_copy"] = pr["frac_of_copy"]
     rec = {"value": round(value, 1), "ms_per_step": round(ms_step, 4), "roofline": roof,
-           "pass_roofline": pass_roofline(kb["survey_pass"], ms_step, ceiling),
+           "pass_roofline": pr,
            "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
            "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s,
            "pass_order": order}
