@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -663,6 +664,61 @@ static void row_pairs(std::vector<int> &cur, size_t base, int G, const std::vect
     cur.swap(out);
 }
 
+// Strips inside a patch (`cur`, ascending index order): on a row-structured numbering (runs of
+// consecutive numbers = the patch's rows) every node gets a column coordinate x -- offsets along its
+// run, each run anchored under the run above through the mesh (the lower-row neighbour of least
+// index of an upper node sits at the upper node's x, as row_pairs aligns its pairs) -- and the patch
+// is walked strip by strip (x in [k*W, (k+1)*W)), each strip top to bottom.  A batch's tiles then
+// reuse the previous row of their strip (2 W nodes x ntracers tiles back with row pairs) instead of
+// the previous row of the whole patch.  No-op unless most of the patch sits in runs of >= W nodes.
+static void strip_order(std::vector<int> &cur, int W, const std::vector<int> &ptr, const std::vector<int> &other)
+{
+    if (W < 2 || cur.size() < (size_t)2 * W) return;
+    std::vector<std::pair<size_t, size_t>> runs;
+    size_t s0 = 0, in_long = 0;
+    for (size_t i = 1; i <= cur.size(); i++)
+        if (i == cur.size() || cur[i] != cur[i - 1] + 1) {
+            runs.emplace_back(s0, i);
+            if (i - s0 >= (size_t)W) in_long += i - s0;
+            s0 = i;
+        }
+    if (runs.size() < 2 || 4 * in_long < 3 * cur.size()) return;
+    const long kNone = std::numeric_limits<long>::min();
+    std::vector<long> x(cur.size(), kNone);
+    for (size_t t = runs[0].first; t < runs[0].second; t++) x[t] = (long)(t - runs[0].first);
+    for (size_t r = 0; r + 1 < runs.size(); r++) {
+        const size_t b0 = runs[r + 1].first, b1 = runs[r + 1].second;
+        const int B0 = cur[b0], nB = (int)(b1 - b0);
+        // anchors: each node of run r with a coordinate places its least neighbour in run r+1
+        for (size_t t = runs[r].first; t < runs[r].second; t++) {
+            if (x[t] == kNone) continue;
+            const int v = cur[t];
+            int first = nB;
+            for (int e = ptr[v]; e < ptr[v + 1]; e++)
+                if (other[e] >= B0 && other[e] < B0 + nB) first = std::min(first, other[e] - B0);
+            if (first < nB && x[b0 + first] == kNone) x[b0 + first] = x[t];
+        }
+        // the rest of the run by offset from its first anchor (a run without one starts at 0)
+        size_t a = b1;
+        for (size_t t = b0; t < b1; t++)
+            if (x[t] != kNone) {
+                a = t;
+                break;
+            }
+        const long xa = a < b1 ? x[a] : 0;
+        if (a == b1) a = b0;
+        for (size_t t = b0; t < b1; t++) x[t] = xa + (long)t - (long)a;
+    }
+    // stable order by (strip, run): floor division for strips left of the first row's start
+    std::vector<size_t> idx(cur.size());
+    for (size_t t = 0; t < idx.size(); t++) idx[t] = t;
+    auto strip_of = [&](size_t t) { return x[t] >= 0 ? x[t] / W : -((-x[t] + W - 1) / W); };
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t p, size_t q) { return strip_of(p) < strip_of(q); });
+    std::vector<int> out(cur.size());
+    for (size_t t = 0; t < idx.size(); t++) out[t] = cur[idx[t]];
+    cur.swap(out);
+}
+
 PlanShape plan_shape(bool batched)
 {
     PlanShape s;
@@ -674,6 +730,7 @@ PlanShape plan_shape(bool batched)
         if (!patch) s.patch = PlanShape::kAuto;
         s.gshift = gs ? atoi(gs) : PlanShape::kAuto;
         s.gcols = gc ? std::max(0, atoi(gc)) : 0;
+        s.strip = knob("FESOM2_BATCH_STRIP", PlanShape::kAuto);  // tuning build: strip width (0 off)
     } else {
         // automatic (the large-partition rule of build_plan) unless the tuning build sets a shape
         s.gshift = knob("FESOM2_GROUP_SHIFT", PlanShape::kAuto);
@@ -727,6 +784,9 @@ ResolvedShape resolve_shape(const PlanShape &shape, long long wet_cells, int nl)
     // cells) -3.5 % per pass, 127k x 47 (6M cells, latency-bound) +2 %
     const char *ienv = getenv("FESOM2_P1V_B3H");
     r.internal = ienv ? atoi(ienv) != 0 : large;
+    // strips inside the patches (batched plan of a large partition): off unless the tuning build
+    // asks (FESOM2_BATCH_STRIP), see strip_order
+    r.strip = shape.strip == PlanShape::kAuto ? 0 : std::max(0, shape.strip);
     return r;
 }
 
@@ -943,6 +1003,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     }
                 } else {
                     std::sort(cur.begin(), cur.end());
+                    if (rs.strip > 0) strip_order(cur, rs.strip, ptr, other);
                     // row pairs on large partitions, with the stash below (1.2M x 80: -2.2 % with 6
                     // columns, 6 tracers -1.2 %)
                     // (tuning: FESOM2_ROWPAIR = R > 1 takes R rows per block)

@@ -194,6 +194,7 @@ struct PlanShape {
     int gshift = 0;  // MeshPlanDev::gshift; kAuto (batched): on partitions of >= 32M wet cells the
                      // largest column count below the natural one with >= 90 % of the lanes busy
     int gcols = 0;   // MeshPlanDev::gcols: columns per block (> 0 overrides gshift)
+    int strip = 0;   // nodes per strip row inside a patch (strip_order; 0: none); kAuto (batched): by size
 };
 // the shape of the single-tracer (batched = false) or the batched plan, with the plan options
 // FESOM2_PATCH / FESOM2_BATCH_PATCH and FESOM2_BATCH_GROUP_SHIFT (read when the plan is built)
@@ -211,10 +212,11 @@ struct ResolvedShape {
     int gcols = 0;          // MeshPlanDev::gcols (0: natural column count << gshift)
     bool large = false;     // row pairs + LDS stash (automatic shape on a large partition)
     bool internal = false;  // block-internal edges limited in p1v (FESOM2_P1V_B3H forces it)
+    int strip = 0;          // strip width inside a patch (strip_order), 0: none
     bool operator==(const ResolvedShape &o) const
     {
         return patch == o.patch && gshift == o.gshift && gcols == o.gcols && large == o.large &&
-               internal == o.internal;
+               internal == o.internal && strip == o.strip;
     }
 };
 long long large_partition_cells();

@@ -3,7 +3,8 @@
 # tuning build: for each variant one timing run of bench.py (the kernels' own HIP events) and one
 # rocprofv3 PMC pass of the L2 -> fabric read requests (profiles/pmc_traffic.py turns them into
 # bytes).  Variants: the default plan; no cluster gathers / no edge gathers (FESOM2_ABLATE 1 / 2,
-# timing only: results wrong); single rows without the stash; row pairs in 1024-node patches.
+# timing only: results wrong); single rows without the stash; row pairs in 1024-node patches;
+# strips of 18 / 24 nodes inside the patches (FESOM2_BATCH_STRIP, strip_order).
 # usage (on the GPU box): bash tools/pmc_batch_ablate.sh TAG [variant ...]
 set -eo pipefail
 tag=${1:-r05}
@@ -16,6 +17,8 @@ declare -A V=(
   [noedge]="FESOM2_ABLATE=2"
   [singlerow]="FESOM2_ROWPAIR=0 FESOM2_P1V_STASH=0"
   [patch1024]="FESOM2_BATCH_PATCH=1024"
+  [strip18]="FESOM2_BATCH_STRIP=18"
+  [strip24]="FESOM2_BATCH_STRIP=24"
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=(default nocluster noedge singlerow patch1024)
