@@ -100,3 +100,33 @@ def test_reference_sequence_variants_match_oracle(knobs, name, monkeypatch):
         st, got = run_pass(m, f, fused=fused)
         assert st == 9
         check_pass(m, got, O.full_pass(m, f))
+
+
+@pytest.mark.parametrize("strip", ["6", "12", "18", "24"])
+@pytest.mark.parametrize("large", [True, False])
+@pytest.mark.parametrize("name,nl", [("structured", 21), ("structured", 48), ("permuted", 21)])
+def test_batched_strip_orders_match_oracle(strip, large, name, nl, monkeypatch):
+    """Round 5: strips inside the batched plan's patches (FESOM2_BATCH_STRIP, strip_order), with the
+    large-partition rules (row pairs, stash, internal edges; FESOM2_LARGE_CELLS=0) and without; a
+    scattered numbering (no rows: strip_order leaves the patch alone).  3 tracers, split pass."""
+    from fesom2_amd import engine, synth
+    monkeypatch.setenv("FESOM2_BATCH_STRIP", strip)
+    if large:
+        monkeypatch.setenv("FESOM2_LARGE_CELLS", "0")
+    g = synth.make_mesh(96, 40, nl, full_depth=nl == 48)
+    m = synth.permute_mesh(g) if name == "permuted" else g
+    tracers = synth.make_tracer_fields(m, 3)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        got = {k: e.download(k).reshape(3, -1) for k in ("del_v", "del_h", "adf_v", "adf_h")}
+        for k in range(3):
+            want = O.full_pass(m, tracers[k])
+            for name_, n in (("adf_v", m.N * m.nl), ("del_v", m.N * m.L), ("del_h", m.N * m.L), ("adf_h", m.E * m.L)):
+                assert (got[name_][k][:n] == want[name_][:n]).all(), (name_, k)
+    finally:
+        e.free()
+        dm.free()
