@@ -811,8 +811,9 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     parallel_check = (args.check and ctx.pool is not None and args.mesh == "structured" and not args.permuted
                       and args.fct_iter == 1)
     cpu_leg = headline and rank == 0 and world == 1 and not args.no_cpu_baseline
-    if parallel_check and not cpu_leg:
-        # the check regenerates its pristine inputs: no second host copy of the fields
+    if parallel_check and not cpu_leg and not mode:
+        # the check regenerates its pristine inputs: no second host copy of the fields (the
+        # transfer legs keep theirs: the step uploads from them)
         e.drop_host()
         del fields, f
         fields = f = None
@@ -1325,6 +1326,8 @@ def main():
                          "this run (N = 1: 127k x 47 with 1 and 6 tracers, 1.2M x 80 with 6 tracers, 9.6M x 80 on "
                          "one GPU; N > 1: 9.6M x 80 split over the N GPUs) as 'extra' sub-records; on: whatever the "
                          "headline workload (e.g. with --exchange host, to rehearse N > 1 on one GPU)")
+    ap.add_argument("--legs", default=None,
+                    help="comma-separated names of the extra legs to run (default: all of them)")
     ap.add_argument("--strong-config", default="9.6M x 80", choices=list(synth.CONFIGS),
                     help="the strong-scaling leg's global mesh (BASELINE configs[4]: 9.6M x 80)")
     ap.add_argument("--comm-timeout", type=float, default=180.0,
@@ -1442,7 +1445,14 @@ def main():
                 out["extra"]["error"] = f"watchdog: '{stage}' not done within its bound"
                 print(json.dumps(out), flush=True)
         ctx.watchdog.on_fire = partial
-        for name, over in extra_legs(args, world):
+        legs = extra_legs(args, world)
+        if args.legs:
+            want = set(args.legs.split(","))
+            unknown = want - {n for n, _ in legs}
+            if unknown:
+                raise SystemExit(f"--legs: unknown {sorted(unknown)}; known {[n for n, _ in legs]}")
+            legs = [(n, o) for n, o in legs if n in want]
+        for name, over in legs:
             la = copy.copy(args)
             for k, v in over.items():
                 setattr(la, k, v)

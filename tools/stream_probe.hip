@@ -179,12 +179,18 @@ int main(int argc, char **argv)
     double copy_tbs = 0, cols_tbs = 0;
     const long cn = nodes * L, cnl = nodes * (L + 1);
     std::vector<double *> bufs;
+    // every array staggered by k x 4352 B from its allocation's start: separately hipMalloc'd
+    // equal-size arrays start on 2 MB boundaries, so element i of each has the same low address bits
+    // and the pattern's streams alias HBM channels -- it then moves 10-15 % less depending on where
+    // the allocator put them (tools/pad_probe.hip): the staggered layout is the stable,
+    // best-placement rate, i.e. the ceiling
     auto alloc = [&](long n) {
         double *p;
-        CHECK(hipMalloc(&p, n * sizeof(double)));
-        CHECK(hipMemset(p, 0, n * sizeof(double)));
+        const size_t skew = ((size_t)bufs.size() * 4352) % 65536;
+        CHECK(hipMalloc(&p, n * sizeof(double) + 65536));
+        CHECK(hipMemset(p, 0, n * sizeof(double) + 65536));
         bufs.push_back(p);
-        return p;
+        return p + skew / sizeof(double);
     };
     Arrays a;
     a.ttf = alloc(cnl);  // room for the padded-stride variant
