@@ -395,10 +395,23 @@ __device__ __forceinline__ void for_edges(const EdgeRef *__restrict__ edges, int
 #pragma unroll
             for (int k = 0; k < kBatch; k++) {
                 const int sl = code[k] >> kStashShift;
-                if (sl)
+                if (!sl) continue;
+                real *sp = stash + (sl - 1) * L + z0;
+                const int lv = edge_lev(code[k]);
+                if constexpr (C == 2) {  // one 16-B LDS store for a full pair (8-B aligned: ds_write2)
+                    if (z0 + 1 < lv) {
+                        f2a_d2u t;
+                        t.x = h[k][0];
+                        t.y = h[k][1];
+                        *reinterpret_cast<f2a_d2u *>(sp) = t;
+                    } else if (z0 < lv) {
+                        sp[0] = h[k][0];
+                    }
+                } else {
 #pragma unroll
                     for (int c = 0; c < C; c++)
-                        if (z0 + c < edge_lev(code[k])) stash[(sl - 1) * L + z0 + c] = h[k][c];
+                        if (z0 + c < lv) sp[c] = h[k][c];
+                }
             }
         }
 #pragma unroll
