@@ -6,6 +6,7 @@ order, so they perform the same IEEE additions as reference.cpp, and the library
 -ffp-contract=off.  Meshes are the synthetic ones of SURVEY.md §8(d) (parity levels: element
 levels uniform in [3, nl]; roofline levels: full depth) and a node/element/edge-permuted variant.
 """
+import ctypes as C
 import os
 
 import numpy as np
@@ -165,6 +166,73 @@ def test_reference_transfer_semantics():
         e.free()
         dm.free()
         abi.set_resident(True)
+
+
+@pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
+def test_producer_upload_mode_two_streams(name):
+    """Round 5: a device-resident host that uploads the producer's fields (and its del_ttf) itself
+    and takes back only del_ttf with fesom2_transfer_back_async_, two tracers on two streams from
+    page-locked arrays (bench.py --transfers producer): every output equals the oracle's, del_ttf in
+    the host arrays; the rebound host pointers are the ones the next transfer uses."""
+    from fesom2_amd import synth
+    m, _ = mesh(name)
+    tracers = synth.make_tracer_fields(m, 2)
+    wants = [O.full_pass(m, t) for t in tracers]
+    streamed = ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")
+    dm = engine.DeviceMesh(m)
+    engines, pins = [], []
+    try:
+        for t in tracers:
+            e = engine.FctAle(dm, t)
+            engines.append(e)
+        hosts = []
+        for k, t in enumerate(tracers):
+            h = {}
+            for name_ in streamed:
+                a, hp = abi.pinned(t[name_].size)
+                a[:] = t[name_]
+                pins.append(hp)
+                h[name_] = a
+            hosts.append(h)
+        # the device copies start poisoned: only the in-step uploads may feed the pass
+        for e in engines:
+            for name_ in streamed:
+                e.upload(name_, np.full(e.size(name_), 7.0))
+        for e, h in zip(engines, hosts):
+            for name_ in streamed:
+                abi.transfer_var_async(e.h[name_], h[name_], e.stream, name_ in ("ttf", "adf_v", "adf_h"))
+            assert e.pre_comm_v() == 7, abi.last_error()
+            assert e.post_comm_h() == 9, abi.last_error()
+            h["del_v"][:] = -1.0  # overwritten by the download below (ordered after the pass)
+            for name_ in ("del_v", "del_h"):
+                abi.transfer_back_async(e.h[name_], h[name_], e.stream)
+        for e in engines:
+            e.sync()
+        for k, (e, h) in enumerate(zip(engines, hosts)):
+            n = m.N * m.L
+            assert np.array_equal(h["del_v"][:n], wants[k]["del_v"][:n]), k
+            assert np.array_equal(h["del_h"][:n], wants[k]["del_h"][:n]), k
+            assert np.array_equal(e.download("adf_h"), wants[k]["adf_h"]), k
+            assert_cols_equal(e.download("plus"), wants[k]["plus"], m.nlev_nod, m.L, m.N, f"plus[{k}]")
+    finally:
+        for e in engines:
+            e.free()
+        dm.free()
+        for hp in pins:
+            abi.free_pinned(hp)
+
+
+def test_transfer_back_async_refuses_a_null_host_array():
+    m, f = mesh("tiny")
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAle(dm, f)
+    try:
+        st = C.c_int(0)
+        abi.dll().fesom2_transfer_back_async_(e.h["del_v"].ref, None, e.stream.ref, C.byref(st))
+        assert st.value == 1 and "no host array" in abi.last_error()
+    finally:
+        e.free()
+        dm.free()
 
 
 def test_invalid_mesh_fails_loudly_without_launch():
