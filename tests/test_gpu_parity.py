@@ -173,7 +173,8 @@ def test_producer_upload_mode_two_streams(name):
     """Round 5: a device-resident host that uploads the producer's fields (and its del_ttf) itself
     and takes back only del_ttf with fesom2_transfer_back_async_, two tracers on two streams from
     page-locked arrays (bench.py --transfers producer): every output equals the oracle's, del_ttf in
-    the host arrays; the rebound host pointers are the ones the next transfer uses."""
+    the host arrays (which held the inputs before: the downloads replaced them); the host writes no
+    pinned array while a transfer from it may be in flight, as FESOM2 would not."""
     from fesom2_amd import synth
     m, _ = mesh(name)
     tracers = synth.make_tracer_fields(m, 2)
@@ -203,7 +204,6 @@ def test_producer_upload_mode_two_streams(name):
                 abi.transfer_var_async(e.h[name_], h[name_], e.stream, name_ in ("ttf", "adf_v", "adf_h"))
             assert e.pre_comm_v() == 7, abi.last_error()
             assert e.post_comm_h() == 9, abi.last_error()
-            h["del_v"][:] = -1.0  # overwritten by the download below (ordered after the pass)
             for name_ in ("del_v", "del_h"):
                 abi.transfer_back_async(e.h[name_], h[name_], e.stream)
         for e in engines:
