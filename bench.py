@@ -1239,6 +1239,17 @@ def extra_legs(args, world):
     return [strong]
 
 
+def select_legs(legs, spec):
+    """The extra legs --legs names (comma-separated; None: all of them, in their order)."""
+    if not spec:
+        return legs
+    want = set(spec.split(","))
+    unknown = want - {n for n, _ in legs}
+    if unknown:
+        raise SystemExit(f"--legs: unknown {sorted(unknown)}; known {[n for n, _ in legs]}")
+    return [(n, o) for n, o in legs if n in want]
+
+
 def compact(rec, args, world):
     """An extra leg's sub-record."""
     m, s = rec["m"], rec["s"]
@@ -1445,14 +1456,7 @@ def main():
                 out["extra"]["error"] = f"watchdog: '{stage}' not done within its bound"
                 print(json.dumps(out), flush=True)
         ctx.watchdog.on_fire = partial
-        legs = extra_legs(args, world)
-        if args.legs:
-            want = set(args.legs.split(","))
-            unknown = want - {n for n, _ in legs}
-            if unknown:
-                raise SystemExit(f"--legs: unknown {sorted(unknown)}; known {[n for n, _ in legs]}")
-            legs = [(n, o) for n, o in legs if n in want]
-        for name, over in legs:
+        for name, over in select_legs(extra_legs(args, world), args.legs):
             la = copy.copy(args)
             for k, v in over.items():
                 setattr(la, k, v)

@@ -318,3 +318,37 @@ def test_reference_byte_models_follow_the_scripts_loops():
     used = int((levels[: m.N] - 1).sum())
     assert got["fct_ale_b2"] == 4 * m.N + 7 * 8 * used
     assert got["fct_ale_c_vertical"] == 4 * m.N + 9 * 8 * used
+
+
+def test_extra_legs_cover_every_baseline_config_and_select():
+    """The default N = 1 run measures configs 1 (1 and 6 tracers), 3, 4's strong base and one rank
+    of its 8-way split, and the two transfer-inclusive modes; N > 1 the strong leg only; --legs
+    picks by name and refuses unknown names."""
+    import argparse
+    a = argparse.Namespace(strong_config="9.6M x 80", steps=20, warmup=5)
+    one = dict(bench.extra_legs(a, 1))
+    assert set(one) == {"config1_127kx47", "config1_127kx47_6tracers", "config3_1p2Mx80_6tracers",
+                        "config4_strong_9p6Mx80", "config4_strong_rank3of8_9p6Mx80",
+                        "config2_transfers_reference", "config2_transfers_producer_2tracers"}
+    assert one["config4_strong_rank3of8_9p6Mx80"]["emulate"] == (3, 8)
+    assert one["config2_transfers_producer_2tracers"]["tracers"] == 2
+    assert [n for n, _ in bench.extra_legs(a, 8)] == ["config4_strong_9p6Mx80"]
+    legs = bench.extra_legs(a, 1)
+    assert bench.select_legs(legs, None) == legs
+    assert [n for n, _ in bench.select_legs(legs, "config3_1p2Mx80_6tracers,config1_127kx47")] == \
+        ["config1_127kx47", "config3_1p2Mx80_6tracers"]
+    with pytest.raises(SystemExit):
+        bench.select_legs(legs, "config9")
+
+
+def test_compact_record_carries_transfers_and_the_emulated_rank():
+    import argparse
+    m = synth.make_mesh(16, 12, 9)
+    rec = {"m": m, "s": bench.mesh_stats(m), "value": 1.0, "ms_per_step": 2.0, "roofline": None,
+           "pass_roofline": {}, "kernels": {"fct_ale_p1v": {"avg_ms": 1.0}}, "check": {"exact": True},
+           "setup_s": 0.1, "pass_order": 0, "transfers": {"h2d_GBps": 30.0}}
+    a = argparse.Namespace(parity_levels=False, mesh="structured", scaling="strong", tracers=1, config="9.6M x 80",
+                           steps=5, warmup=1, emulate=(3, 8))
+    out = bench.compact(rec, a, 1)
+    assert out["transfers"] == {"h2d_GBps": 30.0}
+    assert out["emulated_rank"]["rank"] == 3 and out["emulated_rank"]["of"] == 8
