@@ -19,7 +19,11 @@
 ! mode 3: mode 0's unmodified sequence and transfer semantics in the fast mode: fesom2_set_path_(2)
 !         and fesom2_bind_c_vertical_ once before the step (b3v, cv and the block-internal edges
 !         inside pre_comm, c-horizontal alone in the c-step)
-! Modes 1 and 2 take several tracers at once (FESOM2's tracer loop as one batched call, BASELINE
+! mode 4: device resident with host-side producer fields (bench.py --transfers producer): the
+!         producer's ttf, fct_LO, fct_adf_v, fct_adf_h and the host's del_ttf go up with
+!         transfer_var_async_, the direction-split pass runs, and del_ttf_advvert/advhoriz come back
+!         with fesom2_transfer_back_async_ (the other outputs are downloaded only for the check)
+! Modes 1, 2 and 4 take several tracers at once (FESOM2's tracer loop as one batched call, BASELINE
 ! config 3): ttf, fct_LO, fct_adf_v, fct_adf_h, del_ttf_advvert and del_ttf_advhoriz then hold
 ! ntracers Fortran arrays one after another, (nl-1, nod, ntracers) etc.; ntracers = size(ttf) /
 ! ((myDim+eDim)*(nl-1)).  The mesh fields (area, area_inv, hnode, hnode_new) are shared.
@@ -67,7 +71,7 @@ program fct_ale_host
   call set_mpi_rank(zero, one)
   call make_stream(s, istat)
   call check(istat, "make_stream")
-  if (mode == 1 .or. mode == 2) call fesom2_set_resident(one)
+  if (mode == 1 .or. mode == 2 .or. mode == 4) call fesom2_set_resident(one)
   ! mesh: once per run (reference .cu:114-127)
   call upload_mesh(h_nlev_nod, nlev_nod); call upload_mesh(h_nlev_elem, nlev_elem)
   call upload_mesh(h_elem_nodes, elem_nodes); call upload_mesh(h_nie_num, nie_num)
@@ -114,6 +118,15 @@ program fct_ale_host
       call split_pass()
       call fesom2_graph_end(istat, s, graph); call check(istat, "fesom2_graph_end")
       call fesom2_graph_launch(istat, graph, s); call check(istat, "fesom2_graph_launch")
+    else if (mode == 4) then
+      ! the rest of the host's uploads (ttf, fct_adf_v, fct_adf_h went up above), the pass, and
+      ! del_ttf back into the host arrays on the same stream
+      call transfer_var_async(h_lo, lo, s, no)
+      call transfer_var_async(h_del_v, del_v, s, no)
+      call transfer_var_async(h_del_h, del_h, s, no)
+      call split_pass()
+      call fesom2_transfer_back_async(h_del_v, del_v, s, istat); call check(istat, "fesom2_transfer_back_async")
+      call fesom2_transfer_back_async(h_del_h, del_h, s, istat); call check(istat, "fesom2_transfer_back_async")
     else
       call split_pass()
     end if
@@ -121,7 +134,9 @@ program fct_ale_host
     call check(istat, "await_stream")
     call fesom2_download(h_plus, plus, istat); call fesom2_download(h_minus, minus, istat)
     call fesom2_download(h_adf_v, adf_v, istat); call fesom2_download(h_adf_h, adf_h, istat)
-    call fesom2_download(h_del_v, del_v, istat); call fesom2_download(h_del_h, del_h, istat)
+    if (mode /= 4) then
+      call fesom2_download(h_del_v, del_v, istat); call fesom2_download(h_del_h, del_h, istat)
+    end if
     call check(istat, "fesom2_download")
     if (mode == 2) call fesom2_graph_free(graph)
   end if

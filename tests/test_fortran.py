@@ -91,8 +91,8 @@ def test_input_format_header(tmp_path):
 
 @pytest.mark.gpu
 @needs_flang
-@pytest.mark.parametrize("mode", [0, 1, 2, 3], ids=["reference_sequence", "resident_split", "graph_replay",
-                                                  "reference_sequence_fast_mode"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4], ids=["reference_sequence", "resident_split", "graph_replay",
+                                                     "reference_sequence_fast_mode", "producer_uploads"])
 @pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
 def test_fortran_host_matches_oracle(tmp_path, mode, name):
     import oracle as O
@@ -113,7 +113,7 @@ def test_fortran_host_matches_oracle(tmp_path, mode, name):
 
 @pytest.mark.gpu
 @needs_flang
-@pytest.mark.parametrize("mode", [1, 2], ids=["resident_split", "graph_replay"])
+@pytest.mark.parametrize("mode", [1, 2, 4], ids=["resident_split", "graph_replay", "producer_uploads"])
 @pytest.mark.parametrize("name", ["8k x 20", "127k x 47"])
 def test_fortran_host_batched_tracers(tmp_path, mode, name):
     """FESOM2's tracer loop as one batched call from Fortran (BASELINE config 3's entry points):
