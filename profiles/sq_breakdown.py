@@ -6,7 +6,8 @@ s_waitcnt or a barrier), SQ_WAIT_INST_ANY (ready but stalled at issue) and SQ_AC
 (issuing); the instruction counters give per-wave work.  Counts are averaged over the launches of a
 kernel in the run and printed per launch.
 
-usage: sq_breakdown.py DIR [OUT_JSON]   (DIR = gpurun_out/sq_TAG, holding <workload>_{A,B}/ passes)
+usage: sq_breakdown.py DIR [OUT_JSON]   (DIR = gpurun_out/{sq,mem}_TAG, holding <workload>_{A,B,C}/ passes;
+       tools/sq_breakdown.sh and tools/mem_breakdown.sh)
 """
 import collections
 import csv
@@ -29,7 +30,7 @@ def per_kernel(path):
 def main():
     d = sys.argv[1]
     res = {}
-    for csv_path in sorted(glob.glob(os.path.join(d, "*_[AB]", "**", "*counter_collection.csv"), recursive=True)):
+    for csv_path in sorted(glob.glob(os.path.join(d, "*_[ABC]", "**", "*counter_collection.csv"), recursive=True)):
         wl = os.path.relpath(csv_path, d).split(os.sep)[0].rsplit("_", 1)[0]
         for k, cs in per_kernel(csv_path).items():
             res.setdefault(wl, {}).setdefault(k, {}).update(cs)
@@ -51,6 +52,14 @@ def main():
                                   ("salu_per_wave", "SQ_INSTS_SALU"), ("wave_cycles_per_wave", "SQ_WAVE_CYCLES")):
                     if key in c:
                         row[name] = c[key] / waves
+            def ratio(name, num, den, scale=1.0):
+                if num in c and c.get(den):
+                    row[name] = scale * c[num] / c[den]
+            ratio("l2_read_latency_cycles", "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum")
+            ratio("dram_read_queue_level", "TCC_EA0_RDREQ_LEVEL_sum", "TCC_EA0_RDREQ_sum")
+            if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"]:
+                row["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+            ratio("l1_accesses_per_l2_read", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum")
             if "SQ_LDS_BANK_CONFLICT" in c and "SQ_ACTIVE_INST_LDS" in c and c["SQ_ACTIVE_INST_LDS"]:
                 row["lds_conflict_over_active"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_ACTIVE_INST_LDS"]
             out.setdefault(wl, {})[k] = row
