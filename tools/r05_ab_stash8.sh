@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 5: the LDS-stash p1v form at 64 VGPRs / 8 waves per SIMD (one 16-B LDS store per stashed
 # level pair instead of two 8-B ones: 66 -> 64 VGPRs, no spills) against the previous build
-# (fesom2-accelerate_amd/lib_r05base, 66 VGPRs / 7 waves): parity first, then interleaved A/B of
+# (fesom2-accelerate_amd/lib_r05base: a copy of lib/ built from the commit before, not kept in the tree;
+# 66 VGPRs / 7 waves): parity first, then interleaved A/B of
 # the single-tracer headline, 6 tracers and 9.6M x 80 on one GPU (the forms that take the stash).
 set -eo pipefail
 export TMPDIR=/tmp
