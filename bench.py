@@ -184,6 +184,57 @@ def kernel_bytes_min(s, ntr=1):
             "fct_ale_p1v": 32 * cn + ntr * (64 * cn + 8 * ce)}
 
 
+_CODE_OBJECT = []
+
+
+def engine_code_object():
+    """Code-object hash of the engine library this process runs (fesom2_amd._paths.code_object_hash)."""
+    if not _CODE_OBJECT:
+        from fesom2_amd import _paths
+        _CODE_OBJECT.append(_paths.code_object_hash())
+    return _CODE_OBJECT[0]
+
+
+def traffic_paths(args):
+    """The traffic files that may hold this workload's PMC bytes: --traffic, then
+    profiles/traffic_<config>[_<T>tr | _rank<R>of<N>].json ("127k x 47" -> traffic_127kx47.json)."""
+    slug = args.config.replace(" ", "").replace(".", "p")
+    em = getattr(args, "emulate", None)
+    if em:
+        return [args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}_rank{em[0]}of{em[1]}.json")]
+    return [args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}.json"),
+            os.path.join(ROOT, "profiles", f"traffic_{slug}_{args.tracers}tr.json")]
+
+
+def find_traffic(args, world, dom, code=None):
+    """PMC bytes per launch of kernel `dom` for this workload, and where they came from.  A file
+    matches on workload, tracer count and emulated rank; its bytes are reported only when its
+    `code_object` stamp equals the loaded library's (the kernels it measured are the ones that ran),
+    else traffic is None and the info says `traffic_stale` (a kernel change without a new PMC pass)."""
+    em = getattr(args, "emulate", None)
+    if args.mesh != "structured" or args.parity_levels or args.vlimit != 1 or args.fct_iter != 1 or \
+            args.transfers or not (args.scaling == "weak" or world == 1):
+        return None, {}
+    for path in traffic_paths(args):
+        try:
+            with open(path) as fh:
+                tr = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if tr.get("workload") != args.config or tr.get("tracers", 1) != args.tracers or \
+                tr.get("emulate") != (f"{em[0]}/{em[1]}" if em else None) or \
+                dom not in tr.get("bytes_per_launch", {}):
+            continue
+        code = code or engine_code_object()
+        info = {"traffic_source": os.path.relpath(path, ROOT), "traffic_code_object": tr.get("code_object"),
+                "code_object": code}
+        if tr.get("code_object") != code:
+            info["traffic_stale"] = True
+            return None, info
+        return tr["bytes_per_launch"][dom], info
+    return None, {}
+
+
 # ----------------------------------------------------------------------------- worker pool
 
 def _worker_init():
@@ -348,8 +399,9 @@ def build_local(args, rank, world):
     partition.strip_local_mesh) and its exchange lists."""
     em = getattr(args, "emulate", None)
     if em:  # one rank's strip of a world-way strong split, on this single GPU (halo from global ids)
-        if world > 1 or args.scaling != "strong" or args.mesh != "structured":
-            raise SystemExit("--emulate-rank: 1 GPU, --scaling strong, structured mesh")
+        if world > 1 or args.scaling != "strong" or args.mesh != "structured" or args.permuted:
+            # (its check regenerates the strips in natural order: a permuted numbering would mismatch)
+            raise SystemExit("--emulate-rank: 1 GPU, --scaling strong, structured mesh, natural numbering")
         rank, world = em
     nx, ny, nl = global_dims(args, world)
     if args.mesh != "structured":
@@ -659,17 +711,18 @@ def pcie_probe(nbytes=1 << 30, reps=5):
     pinned array) and both directions at once (transfer_var_async_ and fesom2_transfer_back_async_
     on two streams), 1 GiB each, best of ``reps``."""
     n = nbytes // 8
-    bufs, hps, hs = [], [], []
+    bufs, hps, hs, ss = [], [], [], []
     try:
         for _ in range(2):
             a, hp = abi.pinned(n)
+            hps.append(hp)
             a[:] = 1.0
             h = abi.Handle("pcie")
             abi.check(abi.alloc_var(h, a), "alloc_var_(pcie)")
             bufs.append(a)
-            hps.append(hp)
             hs.append(h)
-        s1, s2 = abi.Stream(), abi.Stream()
+        ss += [abi.Stream(), abi.Stream()]
+        s1, s2 = ss
 
         def best(fn):
             t = []
@@ -689,16 +742,19 @@ def pcie_probe(nbytes=1 << 30, reps=5):
             abi.transfer_var_async(hs[0], bufs[0], s1)
             abi.transfer_back_async(hs[1], bufs[1], s2)
         dup = best(duplex)
-        for h in hs:
-            abi.dll().fesom2_free_(h.ref)
-        for s_ in (s1, s2):
-            abi.dll().fesom2_free_stream_(s_.ref)
         return {"h2d_GBps": round(nbytes / h2d / 1e9, 2), "d2h_GBps": round(nbytes / d2h / 1e9, 2),
                 "duplex_GBps_each_way": round(nbytes / dup / 1e9, 2), "bytes": nbytes,
                 "method": "1 GiB page-locked (allocate_pinned_doubles_) <-> one handle: transfer_var_ (H2D), "
                           "fesom2_download_ (D2H), transfer_var_async_ + fesom2_transfer_back_async_ on two "
                           f"streams at once (duplex); best of {reps}"}
     finally:
+        # on every path: the transfers done, then the handles and streams, then the pinned arrays
+        # the handles point at (an error half-way must not leak 2 GiB of HBM into the later legs)
+        abi.device_sync()
+        for h in hs:
+            abi.dll().fesom2_free_(h.ref)
+        for s_ in ss:
+            abi.dll().fesom2_free_stream_(s_.ref)
         for hp in hps:
             abi.free_pinned(hp)
 
@@ -771,8 +827,9 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     # reference semantics also fct_plus/fct_minus (the host's exchange_nod round trip)
     streamed = ("ttf", "LO", "adf_v", "adf_h", "del_v", "del_h")
     if mode:
-        if world > 1 or getattr(args, "emulate", None) or args.mesh != "structured" or args.fct_iter > 1:
-            raise SystemExit("--transfers: 1 GPU, structured mesh, one FCT iteration")
+        if world > 1 or getattr(args, "emulate", None) or args.mesh != "structured" or args.fct_iter > 1 or \
+                args.permuted:  # (its check regenerates the strips in natural order)
+            raise SystemExit("--transfers: 1 GPU, structured mesh in natural numbering, one FCT iteration")
         if mode == "reference" and args.tracers != 1:
             raise SystemExit("--transfers reference: 1 tracer (the reference's entries take one)")
         if mode == "producer" and args.tracers != 2:
@@ -1014,21 +1071,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
             entry["ref_model_GBps"] = round(refm[name] / (a_ms * 1e-3) / 1e9, 1)
         per_kernel[name] = entry
     dom = max(stats, key=lambda k: stats[k][1]) if stats else None
-    traffic = None
-    slug = args.config.replace(" ", "").replace(".", "p")  # "127k x 47" -> profiles/traffic_127kx47.json
-    for path in (args.traffic, os.path.join(ROOT, "profiles", f"traffic_{slug}.json"),
-                 os.path.join(ROOT, "profiles", f"traffic_{slug}_{args.tracers}tr.json")):
-        try:
-            with open(path) as fh:
-                tr = json.load(fh)
-        except (OSError, ValueError):
-            continue
-        if tr.get("workload") == args.config and tr.get("tracers", 1) == args.tracers and \
-                args.mesh == "structured" and not args.parity_levels and args.vlimit == 1 and \
-                args.fct_iter == 1 and (args.scaling == "weak" or (world == 1 and not getattr(args, "emulate", None))) \
-                and not args.transfers and dom in tr.get("bytes_per_launch", {}):
-            traffic = tr["bytes_per_launch"][dom]
-            break
+    traffic, traffic_info = find_traffic(args, world, dom)
     roof = None
     if dom in kb:
         avg_s = stats[dom][1] / stats[dom][0] * 1e-3
@@ -1043,6 +1086,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
             roof["frac_min"] = round(kbm[dom] / avg_s / HBM_PEAK, 4)
             roof["byte_model_min"] = "alg_bytes_min: SURVEY.md 8(d)'s strict minimum for the same work " \
                                      "(p1v: 32 Cn + ntracers (64 Cn + 8 Ce); p1: 8 Cn + ntracers (40 Cn + 8 Ce))"
+        roof.update(traffic_info)
         if traffic:
             roof["traffic_over_alg"] = round(traffic / kb[dom], 3)
         if ceiling:  # context: what this GPU streams (copy) and streams in p1v's pattern, same run

@@ -808,6 +808,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
     if (m.nlev_nod)
         for (int v = 0; v < n_owned; v++) wet_cells += std::max(m.nlev_nod[v] - 1, 0);
     const ResolvedShape rs = resolve_shape(shape, wet_cells, nl);
+    plan->shape = rs;
+    plan->wet_cells = wet_cells;
     d.gshift = rs.gshift;
     d.gcols = rs.gcols;
     // a large partition: smaller blocks, row-pair blocks and the internal edges' raw flux kept in
@@ -1201,6 +1203,18 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
                 n_owned, n_total, n_edges, nl, with_ring ? h.dim : 0, batched};
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.get();
+    // a batched call whose shape resolves like an existing single-tracer plan's shares that plan (one
+    // build, one set of device arrays; a graph capture after fesom2_prepare_mesh_ finds it either
+    // way): compared with the shape the plan was built with, before any mesh array comes back
+    PlanKey skey = key;
+    std::get<12>(skey) = false;
+    if (batched) {
+        auto si = g_plans.find(skey);
+        if (si != g_plans.end() && si->second->shape == resolve_shape(plan_shape(true), si->second->wet_cells, nl)) {
+            g_plans[key] = si->second;
+            return si->second.get();
+        }
+    }
     if (any_capture()) {  // building a plan copies with hipMemcpy, which would break an open capture
         report("a mesh plan would be built while a graph capture is open: run the sequence once (or "
                "fesom2_prepare_mesh_) before fesom2_graph_begin_");
@@ -1244,22 +1258,13 @@ const Plan *get_plan(const MeshHandles &h, int n_owned, int n_total, int n_edges
         m.nie_num = nnum.data();
         m.dim = h.dim;
     }
-    // a batched call whose shape resolves like the single-tracer one shares that plan (one build,
-    // one set of device arrays; a graph capture after fesom2_prepare_mesh_ finds it either way)
+    // no single-tracer plan yet: a batched call whose shape resolves like the single-tracer one
+    // builds that plan and registers it for both
     bool share = false;
-    PlanKey skey = key;
-    if (batched) {
+    if (batched && g_plans.find(skey) == g_plans.end()) {
         long long wet = 0;
         for (int v : nln) wet += std::max(v - 1, 0);
         share = resolve_shape(plan_shape(true), wet, nl) == resolve_shape(plan_shape(false), wet, nl);
-        std::get<12>(skey) = false;
-        if (share) {
-            auto si = g_plans.find(skey);
-            if (si != g_plans.end()) {
-                g_plans[key] = si->second;
-                return si->second.get();
-            }
-        }
     }
     std::string err;
     std::shared_ptr<Plan> plan = build_plan(m, n_owned, n_total, n_edges, n_owned, nl, plan_shape(batched && !share), err);

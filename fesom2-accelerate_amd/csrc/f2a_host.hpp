@@ -159,6 +159,20 @@ struct HostMesh {  // host views of the connectivity a plan is built from (nullp
     int dim = 0;
 };
 
+struct ResolvedShape {
+    int patch = 0;          // nodes per BFS patch, 0: by numbering (16384 / 4096), 1: index order
+    int gshift = 0;         // MeshPlanDev::gshift
+    int gcols = 0;          // MeshPlanDev::gcols (0: natural column count << gshift)
+    bool large = false;     // row pairs + LDS stash (automatic shape on a large partition)
+    bool internal = false;  // block-internal edges limited in p1v (FESOM2_P1V_B3H forces it)
+    int strip = 0;          // strip width inside a patch (strip_order), 0: none
+    bool operator==(const ResolvedShape &o) const
+    {
+        return patch == o.patch && gshift == o.gshift && gcols == o.gcols && large == o.large &&
+               internal == o.internal && strip == o.strip;
+    }
+};
+
 struct Plan {
     MeshPlanDev dev;
     DeviceArrays mem;
@@ -168,6 +182,11 @@ struct Plan {
     int cache_order = -1;     // plan option FESOM2_CACHE_ORDER: -1 automatic, 0 off, 1 on (pass_order)
     bool has_ring = false;
     int lmax_edges = 0;
+    // what the plan was built for: its resolved shape (under the plan options read at build time)
+    // and the owned wet cells the size rules saw -- a batched call shares a single-tracer plan only
+    // when its own shape resolves to the same (get_plan)
+    ResolvedShape shape;
+    long long wet_cells = 0;
 };
 
 // Tracers::order of a direction-split or fused pass of `ntr` tracers on `plan`.  When the pass's
@@ -206,19 +225,6 @@ PlanShape plan_shape(bool batched);
 // option FESOM2_LARGE_CELLS moves that threshold (tests run the large plan on small meshes with
 // it).  Two shapes that resolve alike give the same plan: get_plan then shares one plan between
 // single-tracer and batched calls (every partition below the threshold).
-struct ResolvedShape {
-    int patch = 0;          // nodes per BFS patch, 0: by numbering (16384 / 4096), 1: index order
-    int gshift = 0;         // MeshPlanDev::gshift
-    int gcols = 0;          // MeshPlanDev::gcols (0: natural column count << gshift)
-    bool large = false;     // row pairs + LDS stash (automatic shape on a large partition)
-    bool internal = false;  // block-internal edges limited in p1v (FESOM2_P1V_B3H forces it)
-    int strip = 0;          // strip width inside a patch (strip_order), 0: none
-    bool operator==(const ResolvedShape &o) const
-    {
-        return patch == o.patch && gshift == o.gshift && gcols == o.gcols && large == o.large &&
-               internal == o.internal && strip == o.strip;
-    }
-};
 long long large_partition_cells();
 ResolvedShape resolve_shape(const PlanShape &s, long long wet_cells, int nl);
 

@@ -146,7 +146,11 @@ bool check_a1(const char *who, int stride, int n_nodes, Buffer *nlev, Buffer *tm
     const Validated key{nlev, nullptr, nlev->serial, nlev->version, 0, 0, n_nodes, stride, 0};
     if (cached_valid(key)) return true;
     std::vector<int> nl;
-    if (!ok(hipStreamSynchronize(s), "hipStreamSynchronize") || !fetch(nlev, nl, n_nodes)) return false;
+    // a cache miss reads the indices back: wait for the whole device, not only `s` -- the upload may
+    // have been enqueued on another (non-blocking) stream, and a check of the old contents would
+    // cache a pass under the new version (once per upload, so the cost stays small)
+    (void)s;
+    if (!ok(hipDeviceSynchronize(), "hipDeviceSynchronize") || !fetch(nlev, nl, n_nodes)) return false;
     for (int n = 0; n < n_nodes; n++)
         if (nl[n] > stride) {
             report("%s: nLevels_nod2D(%d) = %d exceeds maxLevels = %d", who, n + 1, nl[n], stride);
@@ -177,7 +181,8 @@ bool check_a2(const char *who, int stride, int n_elem, Buffer *nlev, Buffer *en,
     const Validated key{nlev, en, nlev->serial, nlev->version, en->serial, en->version, n_elem, stride, nodes};
     if (cached_valid(key)) return true;
     std::vector<int> nl, nodes_of;
-    if (!ok(hipStreamSynchronize(s), "hipStreamSynchronize") || !fetch(nlev, nl, n_elem) ||
+    (void)s;  // (the whole device: see check_a1)
+    if (!ok(hipDeviceSynchronize(), "hipDeviceSynchronize") || !fetch(nlev, nl, n_elem) ||
         !fetch(en, nodes_of, 3 * (size_t)n_elem))
         return false;
     for (int e = 0; e < n_elem; e++) {

@@ -84,6 +84,13 @@ program fct_ale_host
   call reserve_var(h_tmax, NT * L, no, istat); call check(istat, "reserve_var")
   call reserve_var(h_tmin, NT * L, no, istat); call check(istat, "reserve_var")
   call reserve_var(h_uv, 2 * L * T, no, istat); call check(istat, "reserve_var")
+  if (mode == 4) then
+    ! bind (alloc_var_) already copied every field up with the same contents: overwrite the device
+    ! copies of the fields the step uploads with a sentinel, so a missing or misordered in-step
+    ! upload shows in the results (ADVICE r5)
+    call poison(h_ttf, size(ttf)); call poison(h_adf_v, size(adf_v)); call poison(h_adf_h, size(adf_h))
+    call poison(h_lo, size(lo)); call poison(h_del_v, size(del_v)); call poison(h_del_h, size(del_h))
+  end if
   ! per step: the producer's uploads (fct_ale_muscl_LH, reference .cu:269-270)
   call transfer_var_async(h_ttf, ttf, s, yes)
   call transfer_var_async(h_adf_v, adf_v, s, yes)
@@ -157,6 +164,18 @@ contains
         dim, h_edges, h_edge_tri, vlimit, sc(2), sc(3), sc(1))
     call fct_ale_post_comm_h_acc(st(2), s, ntr, nullh, nullh, h_plus, h_minus, h_adf_h, h_del_h, h_area, &
         N, H, E, nl, h_nlev_nod, h_nlev_elem, h_edges, h_edge_tri, sc(1))
+  end subroutine
+
+  subroutine poison(handle, n)
+    type(c_ptr) :: handle
+    integer, intent(in) :: n
+    real(c_double), allocatable :: junk(:)
+    integer(c_int) :: istat
+    allocate(junk(max(n, 1)))
+    junk = 7.0_c_double
+    call fesom2_upload(handle, junk, istat)
+    call check(istat, "fesom2_upload")
+    deallocate(junk)
   end subroutine
 
   subroutine check(istat, what)

@@ -136,6 +136,12 @@ module fesom2_accelerate
       real(c_double) :: host(*)
       integer(c_int) :: istat
     end subroutine
+    subroutine fesom2_upload(handle, host, istat) bind(C, name="fesom2_upload_")
+      import :: c_ptr, c_double, c_int
+      type(c_ptr) :: handle
+      real(c_double) :: host(*)
+      integer(c_int) :: istat
+    end subroutine
     subroutine fesom2_free(handle) bind(C, name="fesom2_free_")
       import :: c_ptr
       type(c_ptr) :: handle

@@ -12,12 +12,21 @@ TCC_EA0_WRREQ_64B_sum = 24.0e6 (x 64 B = 1.536 GB).  So
 
 (the counters include Infinity-Cache hits: this is L2-miss traffic, an upper bound on HBM bytes).
 
-usage: pmc_traffic.py READ_CSV WRITE_CSV WORKLOAD OUT_JSON [TRACERS [SOURCE]]
+Each file is stamped with the code-object hash of the engine library the PMC passes ran
+(``code_object``: sha256 of its .hip_fatbin section, fesom2_amd._paths.code_object_hash) and the
+kernel symbols rocprofv3 reported; bench.py reports the traffic only for a library with the same
+kernels (``traffic_stale`` otherwise).
+
+usage: pmc_traffic.py READ_CSV WRITE_CSV WORKLOAD OUT_JSON [TRACERS [SOURCE]] [--lib SO] [--emulate R/N]
 """
 import collections
+import argparse
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fesom2-accelerate_amd"))
 
 NAMES = {"k_p1": "fct_ale_p1", "k_p1v": "fct_ale_p1v", "k_p2": "fct_ale_p2", "k_p2h": "fct_ale_p2h",
          "k_b3h_g": "fct_ale_b3_horizontal", "k_b3h_u": "fct_ale_b3_horizontal",
@@ -34,19 +43,32 @@ def kernel_key(name):
     return k
 
 
-def per_kernel(path):
+def per_kernel(path, symbols=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
         k = kernel_key(r["Kernel_Name"])
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if symbols is not None:
+            symbols.setdefault(k, set()).add(r["Kernel_Name"].split("(")[0].replace("void ", "").strip())
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
 def main():
-    rd, wr, workload, out = sys.argv[1:5]
-    tracers = int(sys.argv[5]) if len(sys.argv) > 5 else 1
-    source = sys.argv[6] if len(sys.argv) > 6 else ""
-    R, W = per_kernel(rd), per_kernel(wr)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("rd")
+    ap.add_argument("wr")
+    ap.add_argument("workload")
+    ap.add_argument("out")
+    ap.add_argument("tracers", nargs="?", type=int, default=1)
+    ap.add_argument("source", nargs="?", default="")
+    ap.add_argument("--lib", default=None, help="the engine library the passes ran (default: the product build)")
+    ap.add_argument("--emulate", default=None, help="R/N: bench.py --emulate-rank R/N (one rank's strip)")
+    a = ap.parse_args()
+    rd, wr, workload, out, tracers, source = a.rd, a.wr, a.workload, a.out, a.tracers, a.source
+    from fesom2_amd import _paths
+    code = _paths.code_object_hash(a.lib)
+    symbols = {}
+    R, W = per_kernel(rd, symbols), per_kernel(wr, symbols)
     res = {}
     for k, name in NAMES.items():
         if k not in R or k not in W:
@@ -56,10 +78,13 @@ def main():
             32 * r.get("TCC_EA0_RDREQ_32B_sum", 0)
         wb = 64 * w.get("TCC_EA0_WRREQ_64B_sum", 0) + 32 * (w.get("TCC_EA0_WRREQ_sum", 0) -
                                                             w.get("TCC_EA0_WRREQ_64B_sum", 0))
-        res[name] = {"read_bytes": int(rb), "write_bytes": int(wb), "total": int(rb + wb)}
+        res[name] = {"read_bytes": int(rb), "write_bytes": int(wb), "total": int(rb + wb),
+                     "symbol": sorted(symbols.get(k, ()))}
     doc = {"workload": workload, "tracers": tracers, "bytes_per_launch": {k: v["total"] for k, v in res.items()},
            "detail": res, "method": __doc__.strip().splitlines()[0] + " -- see profiles/pmc_traffic.py",
-           "source": source}
+           "source": source, "code_object": code}
+    if a.emulate:
+        doc["emulate"] = a.emulate
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc, indent=1))
 

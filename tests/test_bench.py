@@ -352,3 +352,38 @@ def test_compact_record_carries_transfers_and_the_emulated_rank():
     out = bench.compact(rec, a, 1)
     assert out["transfers"] == {"h2d_GBps": 30.0}
     assert out["emulated_rank"]["rank"] == 3 and out["emulated_rank"]["of"] == 8
+
+
+def test_traffic_is_reported_only_for_the_library_it_measured(tmp_path):
+    """profiles/traffic*.json carry the code-object hash of the library their PMC passes ran: a
+    matching stamp yields the bytes, a mismatched (or missing) one no traffic and traffic_stale, and
+    the emulated-rank leg matches only its own rank's file."""
+    import argparse
+    import json
+    from fesom2_amd import _paths
+    code = _paths.code_object_hash()
+    assert len(code) == 16 and code == _paths.code_object_hash()  # deterministic per build
+    doc = {"workload": "1.2M x 80", "tracers": 1, "bytes_per_launch": {"fct_ale_p1v": 123}, "code_object": code}
+    path = tmp_path / "traffic.json"
+    path.write_text(json.dumps(doc))
+    a = argparse.Namespace(config="1.2M x 80", tracers=1, mesh="structured", parity_levels=False, vlimit=1,
+                           fct_iter=1, transfers=None, scaling="weak", traffic=str(path))
+    got, info = bench.find_traffic(a, 1, "fct_ale_p1v")
+    assert got == 123 and info["traffic_code_object"] == code and "traffic_stale" not in info
+    path.write_text(json.dumps(dict(doc, code_object="0" * 16)))
+    got, info = bench.find_traffic(a, 1, "fct_ale_p1v")
+    assert got is None and info["traffic_stale"] is True and info["code_object"] == code
+    path.write_text(json.dumps({k: v for k, v in doc.items() if k != "code_object"}))
+    assert bench.find_traffic(a, 1, "fct_ale_p1v")[0] is None  # unstamped: stale
+    # another workload, tracer count or kernel: no match at all
+    path.write_text(json.dumps(doc))
+    six = bench.find_traffic(argparse.Namespace(**dict(vars(a), tracers=6)), 1, "fct_ale_p1v")
+    assert six[0] is None or six[1]["traffic_source"] != str(path)  # (the repo's own 6-tracer file may match)
+    assert bench.find_traffic(a, 1, "fct_ale_p2h")[1].get("traffic_source") != str(path)
+    # the emulated rank: only a file stamped with its rank/world
+    e = argparse.Namespace(**dict(vars(a), config="9.6M x 80", scaling="strong", emulate=(3, 8)))
+    path.write_text(json.dumps(dict(doc, workload="9.6M x 80")))
+    assert bench.find_traffic(e, 1, "fct_ale_p1v") == (None, {})
+    path.write_text(json.dumps(dict(doc, workload="9.6M x 80", emulate="3/8")))
+    assert bench.find_traffic(e, 1, "fct_ale_p1v")[0] == 123
+    assert bench.traffic_paths(e)[-1].endswith("traffic_9p6Mx80_rank3of8.json")

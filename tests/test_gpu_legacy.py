@@ -133,3 +133,44 @@ def test_legacy_entries_refuse_levels_beyond_the_stride(prob):
                                True, None)
     assert "elementNodes" in abi.last_error()
     assert np.array_equal(p.host["uv"], p.start["uv"])
+
+
+def test_legacy_check_waits_for_an_upload_on_another_stream(prob):
+    """the index check is cached per (handle, serial, upload version), and the version is
+    bumped when an upload is enqueued.  An upload of bad elementNodes on a second non-blocking stream,
+    queued behind a 512 MB transfer, must still be seen by the next legacy call's check (it waits for
+    the whole device on a cache miss): the call is refused and UV_rhs is never written."""
+    lib = abi.legacy()
+    p, m = prob, prob.m
+    ne = p.ints["en"].size
+    host, hp = abi.pinned((ne + 1) // 2)  # elementNodes as raw bytes in a pinned double array
+    big, bhp = abi.pinned(64 << 20)
+    hen, hbig, s2 = abi.Handle("en"), abi.Handle("big"), abi.Stream()
+    try:
+        host.view(np.int32)[:ne] = p.ints["en"]
+        abi.check(abi.alloc_var(hen, host), "alloc_var_(en)")
+        abi.check(abi.alloc_var(hbig, big), "alloc_var_(big)")
+        abi.dll().transfer_var_(hen.ref, abi.arr(host))
+        en = C.c_void_p(hen.ptr.value)
+        lib.fct_ale_a2_accelerated(p.stride, m.T, p.g("nlev_elem"), en, p.g("uv"), p.g("tmax"), p.g("tmin"),
+                                   True, None)
+        w = {k: v.copy() for k, v in p.start.items()}
+        a2_ref(p.stride, p.ints["nlev_elem"], p.ints["en"], w["tmax"], w["tmin"], w["uv"])
+        assert np.array_equal(p.host["uv"], w["uv"])  # validated (and cached) with the good indices
+        bad = p.ints["en"].copy()
+        bad[4] = m.N + 1
+        host.view(np.int32)[:ne] = bad
+        abi.transfer_var_async(hbig, big, s2)  # keeps s2 busy for a few ms
+        abi.transfer_var_async(hen, host, s2)
+        p.host["uv"][:] = 11.0
+        lib.fct_ale_a2_accelerated(p.stride, m.T, p.g("nlev_elem"), en, p.g("uv"), p.g("tmax"), p.g("tmin"),
+                                   True, None)
+        assert "elementNodes" in abi.last_error()
+        assert np.all(p.host["uv"] == 11.0)
+    finally:
+        s2.sync()
+        for h in (hen, hbig):
+            abi.dll().fesom2_free_(h.ref)
+        s2.free()
+        abi.free_pinned(hp)
+        abi.free_pinned(bhp)

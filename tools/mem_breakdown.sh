@@ -4,9 +4,14 @@
 # (TCC_EA0_RDREQ_LEVEL / TCC_EA0_RDREQ), TA/TD busy and stall cycles -- single tracer against the
 # 6-tracer batch.  Three PMC passes per workload within the per-block limits (<= 4 TCP, 4 TCC, 2 TA,
 # 2 TD, 2 GRBM), no tracing combined; names the box does not list are dropped (rocprofv3 -L).
-# usage (on the GPU box): bash tools/mem_breakdown.sh TAG   -> gpurun_out/mem_TAG/...
+# usage (on the GPU box): bash tools/mem_breakdown.sh TAG ['name|bench args' ...]  -> gpurun_out/mem_TAG/...
+#   default workloads: 1p2M (the headline) and 6tr (--tracers 6); e.g. the 127k x 47 pair:
+#   bash tools/mem_breakdown.sh r06 "127k|--config '127k x 47'" "127k6|--config '127k x 47' --tracers 6"
 set -eo pipefail
 tag=${1:-r05}
+shift || true
+wls=("$@")
+[ ${#wls[@]} -eq 0 ] && wls=("1p2M|" "6tr|--tracers 6")
 export TMPDIR=/tmp
 out=gpurun_out/mem_$tag
 rm -rf "$out" && mkdir -p "$out"
@@ -27,8 +32,10 @@ run() {  # workload pass counters... -- bench args...
 }
 for ps in A B C; do
     eval "ctr=\$$ps"
-    run 1p2M $ps $ctr --
-    run 6tr $ps $ctr -- --tracers 6
+    for w in "${wls[@]}"; do
+        eval "wargs=(${w#*|})"
+        run "${w%%|*}" $ps $ctr -- "${wargs[@]}"
+    done
 done
 find "$out" -name "*.csv" | sort > "$out/files.txt"
 echo "mem breakdown done"

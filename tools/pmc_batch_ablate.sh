@@ -5,7 +5,8 @@
 # bytes).  Variants: the default plan; no cluster gathers / no edge gathers (FESOM2_ABLATE 1 / 2,
 # timing only: results wrong); single rows without the stash; row pairs in 1024-node patches;
 # strips of 18 / 24 nodes inside the patches (FESOM2_BATCH_STRIP, strip_order).
-# usage (on the GPU box): bash tools/pmc_batch_ablate.sh TAG [variant ...]
+# usage (on the GPU box): [ABL_ARGS="--config '127k x 47' --tracers 6"] bash tools/pmc_batch_ablate.sh TAG [variant ...]
+#   (ABL_ARGS: the workload, default --tracers 6)
 set -eo pipefail
 tag=${1:-r05}
 shift || true
@@ -22,7 +23,8 @@ declare -A V=(
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=(default nocluster noedge singlerow patch1024)
-args=(--tracers 6 --no-cpu-baseline --no-check --extras none)
+eval "wl=(${ABL_ARGS:---tracers 6})"
+args=("${wl[@]}" --no-cpu-baseline --no-check --extras none)
 for v in "${names[@]}"; do
   out=gpurun_out/pmcab_${tag}_$v
   rm -rf "$out" && mkdir -p "$out"
