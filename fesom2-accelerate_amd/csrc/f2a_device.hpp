@@ -30,16 +30,22 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 //   c_tile_rev      FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range
 //                   backwards, so it starts on the data the previous kernel touched last (still in the
 //                   Infinity Cache); the product takes the direction per call (Tracers::order)
+//   c_tracer_group  FESOM2_TRACER_GROUP = g (batched tracers, tracer-fastest kernels): tiles run in
+//                   groups of g tracers -- every column group for tracers 0..g-1, then g..2g-1 -- so a
+//                   column's reuse by the next patch row comes g, not ntracers, tiles later per column;
+//                   overrides the per-call Tracers::group (0: the call's)
 #if F2A_TUNING
 static __constant__ int c_xcd_swizzle = 1;
 static __constant__ int c_ablate = 0;
 static __constant__ int c_tracer_major = 2;
 static __constant__ int c_tile_rev = 0;
+static __constant__ int c_tracer_group = 0;
 #else
 static constexpr int c_xcd_swizzle = 1;
 static constexpr int c_ablate = 0;
 static constexpr int c_tracer_major = 2;
 static constexpr int c_tile_rev = 0;
+static constexpr int c_tracer_group = 0;
 #endif
 
 __device__ __forceinline__ int xcd_tile(int b, int G)
@@ -75,6 +81,8 @@ static void init_swizzle()
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ablate), &v, sizeof v);
     if (const int v = knob("FESOM2_TILE_REV", 0); v != 0)
         (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tile_rev), &v, sizeof v);
+    if (const int v = knob("FESOM2_TRACER_GROUP", 0); v != 0)
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_group), &v, sizeof v);
 #endif
 }
 
@@ -154,7 +162,9 @@ __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDi
 // tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
 // for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
 // keep the L2 to themselves)
-__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false, bool rev = false)
+// (gsz > 1: tiles in groups of gsz tracers -- Tracers::group -- every column group of tracers
+// 0..gsz-1 first, then the next gsz; the tuning build's FESOM2_TRACER_GROUP overrides it)
+__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false, bool rev = false, int gsz = 0)
 {
     const int t = rev ? xcd_tile_rev(blockIdx.x, gridDim.x) : block_tile();
     if (ntr == 1) {
@@ -165,6 +175,13 @@ __device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false
         const int groups = gridDim.x / ntr;
         tr = t / groups;
         return t - tr * groups;
+    }
+    const int gs = c_tracer_group ? c_tracer_group : gsz;
+    if (gs > 1 && gs < ntr && ntr % gs == 0) {
+        const int span = gridDim.x / ntr * gs;  // tiles of one tracer group
+        const int tg = t / span, rem = t - tg * span, g = rem / gs;
+        tr = tg * gs + (rem - g * gs);
+        return g;
     }
     const int g = t / ntr;
     tr = t - g * ntr;
@@ -340,7 +357,7 @@ __device__ __forceinline__ void cluster_bound(const RingRef *__restrict__ ring, 
         for (int k = 0; k < kBatch; k++) {
             const RingRef rr = (r + k < r1) ? ring[r + k] : RingRef{0, 0};
             idx[k] = (size_t)rr.node * L + zl;
-            lev[k] = rr.lev;
+            lev[k] = rr.lev & kLevMask;  // (above it: the p1v block's union slot, MeshPlanDev::cu_ptr)
         }
         real lo[kBatch][C], tt[kBatch][C];
 #pragma unroll

@@ -586,6 +586,12 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }
 
+int tracer_group(const Plan &plan, int ntr)
+{
+    if (plan.dev.cu_G <= 0 || ntr < 4) return 0;
+    return ntr % 3 == 0 ? 3 : ntr % 2 == 0 ? 2 : 0;
+}
+
 int pass_order(const Plan &plan, int ntr)
 {
     const MeshPlanDev &d = plan.dev;
@@ -787,6 +793,22 @@ ResolvedShape resolve_shape(const PlanShape &shape, long long wet_cells, int nl)
     // strips inside the patches (batched plan of a large partition): off unless the tuning build
     // asks (FESOM2_BATCH_STRIP), see strip_order
     r.strip = shape.strip == PlanShape::kAuto ? 0 : std::max(0, shape.strip);
+    // cluster unions (MeshPlanDev::cu_ptr) in row-pair blocks on small partitions: p1v stages each
+    // block's union of cluster columns into LDS once instead of gathering every column's cluster.
+    // Measured at 127k x 47 (24 level pairs): 6 tracers -11 % per pass with the tracer groups
+    // (tracer_group), 1 tracer -3 to -7 %; at 1.2M x 80 (large partitions) +9 to +50 % -- the LDS
+    // images cost occupancy there.  The cap keeps the images to 16 KB per block (21 columns at L =
+    // 47: the 4 x 2 blocks' unions hold 22, the last one gathered from memory).  Plan option
+    // FESOM2_P1V_UNION: 0 off, unset automatic (small partitions, L <= 64), > 0 on (the tuning
+    // build: 1 or 2 also picks the kernel's LDS layout)
+    const char *uenv = getenv("FESOM2_P1V_UNION");
+    const int S = p1v_slots(nl);
+    const bool want = uenv ? atoi(uenv) != 0 : (!large && nl - 1 <= 64);
+    if (want) {
+        const int G = p1v_group_columns(nl, r.gshift, r.gcols);
+        r.union_cap = std::max(G, (int)(16384 / (2 * 2 * (size_t)S * sizeof(real))));
+        if (const int k = knob("FESOM2_P1V_UNION_MAX", 0); k > 0) r.union_cap = std::max(G, k);
+    }
     return r;
 }
 
@@ -1009,7 +1031,7 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     // row pairs on large partitions, with the stash below (1.2M x 80: -2.2 % with 6
                     // columns, 6 tracers -1.2 %)
                     // (tuning: FESOM2_ROWPAIR = R > 1 takes R rows per block)
-                    if (const int rp = knob("FESOM2_ROWPAIR", large_auto ? 1 : 0))
+                    if (const int rp = knob("FESOM2_ROWPAIR", (large_auto || rs.union_cap > 0) ? 1 : 0))
                         row_pairs(cur, order.size(), p1v_group_columns(nl, d.gshift, d.gcols), ptr, other,
                                   rp > 1 ? rp : 2);
                 }
@@ -1044,6 +1066,61 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             }
             ni.r1 = (int)pring.size();
             ni.zdry = with_ring ? zdry[n] : 0;
+        }
+        // the cluster union of every p1v block (ResolvedShape::union_cap; see MeshPlanDev::cu_ptr):
+        // its own columns first, then the other cluster nodes in order of first use; each RingRef of
+        // the processing-order copies gets its slot in the union above the level count.  Skipped
+        // when a union would exceed the block's threads (one id each) or 64 KB of LDS images.
+        if (with_ring && rs.union_cap > 0 && L <= kLevMask) {
+            const int UG = p1v_group_columns(nl, d.gshift, d.gcols), S = p1v_slots(nl);
+            // at most `cap` nodes per union (never fewer than the block's own columns): the cluster
+            // nodes past it keep slot 0, and p1v gathers those from memory
+            const int cap = std::max(UG, rs.union_cap);
+            std::vector<int> sizes;
+            const int nblk = (n_owned + UG - 1) / UG;
+            std::vector<int> cptr(nblk + 1, 0), cnode;
+            std::vector<RingRef> enc(pring);
+            std::vector<int> slot_of_node(n_total, -1);
+            int most = 0;
+            for (int b = 0; b < nblk; b++) {
+                const int k0 = b * UG, k1 = std::min(n_owned, k0 + UG);
+                const size_t base = cnode.size();
+                for (int k = k0; k < k1; k++) {
+                    slot_of_node[info[k].n] = k - k0;
+                    cnode.push_back(info[k].n);
+                }
+                for (int k = k0; k < k1; k++)
+                    for (int r = info[k].r0; r < info[k].r1; r++) {
+                        int &sl = slot_of_node[pring[r].node];
+                        if (sl < 0 && (int)(cnode.size() - base) < cap) {
+                            sl = (int)(cnode.size() - base);
+                            cnode.push_back(pring[r].node);
+                        }
+                        enc[r].lev = pring[r].lev | (sl >= 0 ? (sl + 1) << kStashShift : 0);
+                    }
+                for (size_t q = base; q < cnode.size(); q++) slot_of_node[cnode[q]] = -1;
+                cptr[b + 1] = (int)cnode.size();
+                most = std::max(most, (int)(cnode.size() - base));
+                sizes.push_back((int)(cnode.size() - base));
+            }
+            const int threads = (UG * S + 63) / 64 * 64;
+            if (most <= threads && 2 * (size_t)most * 2 * S * sizeof(real) <= 65536) {
+                pring.swap(enc);
+                d.cu_G = UG;
+                d.cu_max = most;
+                d.cu_ptr = plan->mem.upload(cptr);
+                d.cu_node = plan->mem.upload(cnode);
+                if (!d.cu_ptr || !d.cu_node) return fail("device allocation for the cluster unions failed");
+            }
+            if (knob("FESOM2_PLAN_STATS", 0) && !sizes.empty()) {
+                long outside = 0;
+                for (const RingRef &rr : pring) outside += (rr.lev >> kStashShift) == 0;
+                std::sort(sizes.begin(), sizes.end());
+                fprintf(stderr, "fesom2-accelerate: p1v G=%d cluster unions: %zu nodes over %d blocks (p50 %d, p90 %d, "
+                        "p99 %d, max %d; cap %d), %zu ring entries, %ld outside a union\n", UG, cnode.size(), nblk,
+                        sizes[sizes.size() / 2], sizes[sizes.size() * 9 / 10], sizes[sizes.size() * 99 / 100], most,
+                        cap, pring.size(), outside);
+            }
         }
         // edges in the order of their first visited endpoint (edges without an owned endpoint last)
         std::vector<int4> einfo;

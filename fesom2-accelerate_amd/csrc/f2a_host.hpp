@@ -166,10 +166,11 @@ struct ResolvedShape {
     bool large = false;     // row pairs + LDS stash (automatic shape on a large partition)
     bool internal = false;  // block-internal edges limited in p1v (FESOM2_P1V_B3H forces it)
     int strip = 0;          // strip width inside a patch (strip_order), 0: none
+    int union_cap = 0;      // > 0: cluster unions of at most this many columns per p1v block, in row pairs
     bool operator==(const ResolvedShape &o) const
     {
         return patch == o.patch && gshift == o.gshift && gcols == o.gcols && large == o.large &&
-               internal == o.internal && strip == o.strip;
+               internal == o.internal && strip == o.strip && union_cap == o.union_cap;
     }
 };
 
@@ -199,6 +200,10 @@ struct Plan {
 // every kernel forwards with non-temporal flux stores (measured).
 constexpr long long kCacheOrderBytes = 192ll << 20;
 int pass_order(const Plan &plan, int ntr);
+// Tracers::group of a batched call of `ntr` tracers on `plan`: on a plan with cluster unions (small
+// partitions) the tracer-fastest kernels tile 3 (or 2) tracers at a time -- measured with the unions
+// at 6 x 127k x 47 -- else every tracer interleaved (0)
+int tracer_group(const Plan &plan, int ntr);
 
 // Processing-order options of a plan.  Single-tracer calls use the defaults (16384-node patches
 // for a numbering with locality, the natural block size); calls with ntracers > 1 get a plan of

@@ -166,6 +166,15 @@ struct MeshPlanDev {
     int int_stash = 0;
     const int *int_ptr = nullptr;
     const int4 *int_edges = nullptr;
+    // cluster union of each p1v block (the tuning build's FESOM2_P1V_UNION): block b's distinct
+    // cluster nodes cu_node[cu_ptr[b] .. cu_ptr[b+1]), its own columns first (slot j = column j);
+    // every processing-order RingRef then carries (slot + 1) << kStashShift above its level count,
+    // and p1v stages the union's LO/ttf columns into LDS once per block (global -> LDS DMA) instead
+    // of gathering each column's cluster separately
+    int cu_G = 0;    // p1v columns per block the lists were built for (0: none)
+    int cu_max = 0;  // most union nodes of one block
+    const int *cu_ptr = nullptr;
+    const int *cu_node = nullptr;
     // phase-2 node records: interior nodes (every incident edge interior) first, then boundary
     // nodes; interior work needs no halo values, so it can overlap the halo exchange
     const NodeRec *p2_rec = nullptr;      // [n_owned]
@@ -184,6 +193,9 @@ struct Tracers {
     // pass order (pass_order, f2a_host.hpp): bit 0 the p1 kernels and bit 2 the p2 node kernels
     // walk each XCD's tile range backwards, bit 3 b3h stores the limited fluxes cache-allocating
     int order = 0;
+    // tracer-fastest kernels (p1, p2h): tiles in groups of `group` tracers (0: all interleaved),
+    // see tracer_group (f2a_host.hpp)
+    int group = 0;
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().
@@ -225,6 +237,12 @@ inline size_t p1_lds_bytes(int G, int L, int vlimit, bool internal)
 {
     return (2 + (vlimit != 1 ? 1 : 0)) * (size_t)G * L * sizeof(double) + (size_t)G * 192 +
            (internal ? p1_internal_lds_bytes() : 0);
+}
+// the cluster-union staging behind `base` bytes of a p1v block's LDS (MeshPlanDev::cu_ptr): 16-byte
+// aligned LO | ttf images of cu_max columns of 2S doubles (S level-pair slots), then the node ids
+inline size_t p1_union_lds_bytes(size_t base, int cu_max, int S)
+{
+    return (base + 15) / 16 * 16 + 2 * (size_t)cu_max * 2 * S * sizeof(double) + (size_t)cu_max * sizeof(int);
 }
 
 struct P2Args {

@@ -326,13 +326,18 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
     int tr = 0;
-    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, (c_tile_rev | a0.tr.order) & 1);
+    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, (c_tile_rev | a0.tr.order) & 1, a0.tr.group);
     const int first = grp * G;
     const int ncol = min(G, a0.n_owned - first);
+    // doubles in front of the records: tvert max | min, or (OPT & 1024) the larger of that and the
+    // cluster union's LO | ttf images, which then share the region (tvert is written after the union
+    // has been read)
+    int R0 = 2 * G * L;
+    if constexpr ((OPT & 1024) != 0) R0 = max(R0, 2 * mp.cu_max * 2 * S);
     // OPT & 16 (VERT): the block-internal edges (both endpoints among its columns) are limited here,
     // after b2, from the plus/minus in LDS.  Wave 0 stages their entries and slot offsets (one
     // per lane, exclusive scan of ceil(lev/C)) while the records load.
-    int4 *ie_ent = reinterpret_cast<int4 *>(lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)));
+    int4 *ie_ent = reinterpret_cast<int4 *>(lds + R0 + G * (int)(sizeof(NodeRec) / sizeof(real)));
     int *ie_off = reinterpret_cast<int *>(ie_ent + kMaxInternal);  // [kMaxInternal + 1]: + total
     // OPT & 32: the entries go global -> LDS by DMA after the records barrier instead (no VGPRs, off
     // the records' critical path: the two dependent loads above delay the block's first barrier),
@@ -363,7 +368,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     }
     // VLIMIT 2/3: max(LO, ttf) of the own column, for the 3-point vertical bound after the barrier
     // (behind the records and the internal-edge staging: p1_lds_bytes)
-    real *cmx = lds + 2 * G * L + G * (int)(sizeof(NodeRec) / sizeof(real)) +
+    real *cmx = lds + R0 + G * (int)(sizeof(NodeRec) / sizeof(real)) +
                 ((VERT && (OPT & 16)) ? (int)(p1_internal_lds_bytes() / sizeof(real)) : 0);
     // OPT & 256 (with OPT & 16; the product default on large partitions, MeshPlanDev::int_stash; the
     // tuning build's FESOM2_P1V_STASH forces it): the internal edges' raw flux, kept by the first
@@ -371,7 +376,27 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     real *stash = nullptr;
     if constexpr (VERT && (OPT & 16) && (OPT & 256))
         stash = cmx + (VLIMIT != 1 ? G * L : 0);
-    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + 2 * G * L);
+    // OPT & 512 (MeshPlanDev::cu_ptr): the block's cluster union -- node ids, then the LO | ttf images
+    // of its columns (2S doubles each, 16-byte aligned, behind every other region: p1_union_lds_bytes)
+    real *uLO = nullptr, *uTT = nullptr;
+    int *u_node = nullptr;
+    int nU = 0;
+    if constexpr ((OPT & 512) != 0) {
+        const size_t off = (size_t)(cmx - lds) + (VLIMIT != 1 ? (size_t)G * L : 0) +
+                           (((OPT & 16) && (OPT & 256)) ? (size_t)mp.int_max * L : 0);
+        if constexpr ((OPT & 1024) != 0) {  // the images in front (R0), the ids behind everything
+            uLO = lds;
+            u_node = reinterpret_cast<int *>(lds + off);
+        } else {
+            uLO = lds + (off + 1) / 2 * 2;
+            u_node = reinterpret_cast<int *>(uLO + 2 * (size_t)mp.cu_max * 2 * S);
+        }
+        const int blk = first / G, c0 = mp.cu_ptr[blk];
+        nU = mp.cu_ptr[blk + 1] - c0;
+        uTT = uLO + (size_t)nU * 2 * S;
+        if (t < nU) u_node[t] = mp.cu_node[c0 + t];  // (read after stage_records' barrier)
+    }
+    const NodeRec *recs = stage_records(mp.node_rec, first, ncol, lds + R0);
     if constexpr (VERT && (OPT & 16) && (OPT & 32)) {
         if (t < int_n)  // wave 0 (int_n <= kMaxInternal = kWave): lane t's entry lands at ie_ent[t]
             __builtin_amdgcn_global_load_lds(
@@ -392,6 +417,21 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         a.adf_v += tr * a.tr.lev;
         a.adf_h += tr * a.tr.edge;
         if (VERT && !(OPT & 64)) a.del_v += tr * a.tr.node;
+    }
+    if constexpr ((OPT & 512) != 0) {
+        // the union's LO and ttf columns global -> LDS, 16 B per lane: item f of [array][slot][pair]
+        // lands at uLO + 2f, i.e. each wave's 64 items fill 1 KB of LDS (landed at the next barrier)
+        const int per = nU * S, items = 2 * per;
+        for (int f0 = (t >> 6) * kWave; f0 < items; f0 += (int)blockDim.x) {
+            const int f = f0 + (t & (kWave - 1));
+            if (f < items) {
+                const int arr = f >= per ? 1 : 0, g = f - arr * per;
+                const int sl = (int)(((float)g + 0.5f) * invS), pr = g - sl * S;
+                const real *src = (arr ? a.ttf : a.LO) + (size_t)u_node[sl] * L + 2 * pr;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(uLO + 2 * f0), 16, 0, 0);
+            }
+        }
     }
     const NodeRec &rec = recs[j];
     NodeInfo ni{};
@@ -436,6 +476,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
             vx[c] = dry ? -a.big : -INFINITY;
             vn[c] = dry ? a.big : INFINITY;
         }
+        if constexpr ((OPT & 512) == 0) {
         const size_t bl = b;  // (odd L: the last slot's pair reads one level past the column, ldo)
         ldo_pre<C, ODD>(a.LO + bl, lo, last1);  // the own column: cluster bound (self last in the ring), b2, cv
         ldo_pre<C, ODD>(a.ttf + bl, tt, last1);
@@ -449,6 +490,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         cluster_bound<C, RB, ODD>(rec.ring, 0, min(no, kRecRing), a.LO, a.ttf, z0, L, vx, vn, last1);
         if (no > kRecRing)
             cluster_bound<C, RB, ODD>(mp.p_ring, ni.r0 + kRecRing, ni.r0 + no, a.LO, a.ttf, z0, L, vx, vn, last1);
+        }
         auto add = [&](int c, real h, int second) {
             if (second) {  // ascending edge order: the reference's sum order (reference.cpp:406-425)
                 p[c] += RMAX(0., -h);
@@ -461,6 +503,51 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
         for_edges<C, EB, ODD>(rec.edge, 0, min(ne, kRecEdge), a.adf_h, z0, L, add, last1, stash);
         if (ne > kRecEdge)
             for_edges<C, EB, ODD>(mp.p_edges, ni.e0 + kRecEdge, ni.e1, a.adf_h, z0, L, add, last1, stash);
+    }
+    if constexpr ((OPT & 512) != 0) {
+        // the union landed: own LO/ttf from slot j, the cluster bound from the slots the ring entries
+        // carry -- the same values combined in the same order as the gathers above
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA writes done before the barrier publishes them
+        __syncthreads();
+        if (nw > 0) {
+            const int S2 = 2 * S;
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                lo[c] = uLO[j * S2 + z0 + c];
+                tt[c] = uTT[j * S2 + z0 + c];
+            }
+            const int nr = (c_ablate & 1) ? 0 : ni.r1 - ni.r0;
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                if (nr > 0 && z0 + c < ni.self_lev) {
+                    vx[c] = RMAX(vx[c], RMAX(lo[c], tt[c]));
+                    vn[c] = RMIN(vn[c], RMIN(lo[c], tt[c]));
+                }
+            const int no = nr > 0 ? nr - 1 : 0;
+            for (int r = 0; r < no; r++) {
+                const RingRef rr = r < kRecRing ? rec.ring[r] : mp.p_ring[ni.r0 + r];
+                const int lv = rr.lev & kLevMask, sl = (rr.lev >> kStashShift) - 1;
+                if (z0 >= lv) continue;
+                real l2[C], t2[C];
+                if (sl >= 0) {
+#pragma unroll
+                    for (int c = 0; c < C; c++) {
+                        l2[c] = uLO[sl * S2 + z0 + c];
+                        t2[c] = uTT[sl * S2 + z0 + c];
+                    }
+                } else {  // past the union's cap (MeshPlanDev::cu_max): from memory
+                    ldo_pre<C, ODD>(a.LO + (size_t)rr.node * L + z0, l2, last1);
+                    ldo_pre<C, ODD>(a.ttf + (size_t)rr.node * L + z0, t2, last1);
+                }
+#pragma unroll
+                for (int c = 0; c < C; c++)
+                    if (z0 + c < lv) {
+                        vx[c] = RMAX(vx[c], RMAX(l2[c], t2[c]));
+                        vn[c] = RMIN(vn[c], RMIN(l2[c], t2[c]));
+                    }
+            }
+        }
+        if constexpr ((OPT & 1024) != 0) __syncthreads();  // every union read done: tvert takes the region
     }
     real *tvx = lds, *tvn = lds + G * L;
     const int q = j * L + z0;
@@ -670,7 +757,7 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = (L + C - 1) / C;
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4, a.tr.group) * G;
     if (tr) {
         a.del_h += tr * a.tr.node;
         a.adf_h += tr * a.tr.edge;
@@ -945,7 +1032,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
 {
     extern __shared__ real lds[];  // NodeRec[G]
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4, a.tr.group) * G;
     if (tr) {
         a.plus += tr * a.tr.node;
         a.minus += tr * a.tr.node;
@@ -1441,6 +1528,39 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
 #undef F2A_P1B
         }
     }
+    // FESOM2_P1V_UNION = 1 (plan built with the cluster unions, MeshPlanDev::cu_ptr): the union's
+    // LO/ttf columns staged into LDS once per block instead of each column's cluster gathers
+    if (mp.cu_G > 0 && mp.cu_ptr && a.vlimit == 1) {
+        const int L = a.nl - 1;
+        const bool odd = odd_pairs(L);
+        if (odd || levels_per_thread(L) == 2) {
+            const int S = (L + 1) / 2, G = plan_columns(S, mp);
+            if (G == mp.cu_G) {
+                const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+                const bool st = mp.int_stash && in;
+                const size_t base = p1_lds_bytes(G, L, 1, in) + (st ? (size_t)mp.int_max * L * sizeof(real) : 0);
+                const float inv = 1.0f / (float)S;
+                if (knob("FESOM2_P1V_UNION", 2) != 1) {  // the union images share tvert's region (OPT 1024)
+                    const size_t tv = 2 * (size_t)G * L * sizeof(real);
+                    const size_t lds = std::max(tv, 2 * (size_t)mp.cu_max * 2 * S * sizeof(real)) + (base - tv) +
+                                       (size_t)mp.cu_max * sizeof(int);
+                    if (st && odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+                    if (st) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+                    if (in && odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+                    if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+                    if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+                    F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+                }
+                const size_t lds = p1_union_lds_bytes(base, mp.cu_max, S);
+                if (st && odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+                if (st) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+                if (in && odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+                if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+                if (odd) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512, true>), groups, G, S, lds, s, mp, a, G, inv);
+                F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 512>), groups, G, S, lds, s, mp, a, G, inv);
+            }
+        }
+    }
     // FESOM2_P1V_STASH = 1 (plan built with the stash marks): the internal-edge forms keep the
     // internal edges' raw flux from b1h in LDS (int_max x L doubles more) instead of re-reading it
     if (mp.int_stash && in && a.vlimit == 1) {
@@ -1486,8 +1606,28 @@ hipError_t launch_p1v(const MeshPlanDev &mp, const P1Args &a, hipStream_t s)
     const int L = a.nl - 1;
     // OPT 4: 16-byte loads/stores of the stride-nl arrays; +16 the block-internal edges'
     // b3-horizontal, +32 their entries staged into LDS by DMA, +256 their raw flux kept in LDS by
-    // the b1h gather (plans with MeshPlanDev::int_stash: batched calls on large partitions).  NT: the
-    // single-use streams (plus/minus/del_v stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
+    // the b1h gather (plans with MeshPlanDev::int_stash: batched calls on large partitions), +512
+    // the block's cluster union staged into LDS by DMA (plans with MeshPlanDev::cu_ptr: small
+    // partitions), +1024 its images in tvert's region.  NT: the single-use streams (plus/minus/del_v
+    // stores, the tail's del_v/hnode/hnode_new loads) non-temporal.
+    if (mp.cu_G > 0 && mp.cu_ptr && a.vlimit == 1 && (odd_pairs(L) || levels_per_thread(L) == 2)) {
+        const int S = (L + 1) / 2, G = plan_columns(S, mp);
+        if (G == mp.cu_G) {
+            const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;
+            const bool st = mp.int_stash && in;
+            const size_t base = p1_lds_bytes(G, L, 1, in) + (st ? (size_t)mp.int_max * L * sizeof(real) : 0);
+            const size_t tv = 2 * (size_t)G * L * sizeof(real);
+            const size_t lds = std::max(tv, 2 * (size_t)mp.cu_max * 2 * S * sizeof(real)) + (base - tv) +
+                               (size_t)mp.cu_max * sizeof(int);
+            const float inv = 1.0f / (float)S;
+            if (st && odd_pairs(L)) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (st) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 256 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+            if (in && odd_pairs(L)) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+            if (in) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 52 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+            if (odd_pairs(L)) F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 1536, true>), groups, G, S, lds, s, mp, a, G, inv);
+            F2A_LAUNCH_GROUPS((k_p1<1, 2, 2, 2, true, true, 4 | 1536>), groups, G, S, lds, s, mp, a, G, inv);
+        }
+    }
     if (mp.int_stash && in && a.vlimit == 1 && (odd_pairs(L) || levels_per_thread(L) == 2)) {
         const int S = (L + 1) / 2, G = plan_columns(S, mp);
         const long groups = (long)(a.n_owned + G - 1) / G * a.tr.n;

@@ -78,7 +78,7 @@ def test_product_library_reads_only_the_plan_options():
     names = set(re.findall(rb"FESOM2_[A-Z0-9_]+", data))
     assert names <= {b"FESOM2_PATH", b"FESOM2_NUM_KERNELS", b"FESOM2_P1V_B3H", b"FESOM2_PATCH",
                      b"FESOM2_BATCH_PATCH", b"FESOM2_BATCH_GROUP_SHIFT", b"FESOM2_BATCH_GROUP",
-                     b"FESOM2_CACHE_ORDER", b"FESOM2_LARGE_CELLS"}, names
+                     b"FESOM2_CACHE_ORDER", b"FESOM2_LARGE_CELLS", b"FESOM2_P1V_UNION"}, names
     syms = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True, check=True).stdout
     for k in ("k_p2w", "k_p2f", "k_p1e", "k_p1s", "k_p2hf", "k_b3h_n", "k_p1p", "k_p1t", "launch_p1_variant"):
         assert not re.search(rf"\b{k}\b", syms), k

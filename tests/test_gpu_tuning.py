@@ -130,3 +130,72 @@ def test_batched_strip_orders_match_oracle(strip, large, name, nl, monkeypatch):
     finally:
         e.free()
         dm.free()
+
+
+@pytest.mark.parametrize("mode,cap", [("1", ""), ("2", ""), ("2", "1"), ("2", "12")])
+@pytest.mark.parametrize("ntr", [1, 3])
+@pytest.mark.parametrize("large", [True, False])
+@pytest.mark.parametrize("name,nl", [("structured", 21), ("structured", 48), ("permuted", 21),
+                                     ("delaunay", 21), ("delaunay", 48)])
+def test_cluster_union_staging_matches_oracle(mode, cap, ntr, large, name, nl, monkeypatch):
+    """Round 6: p1v with each block's cluster union staged into LDS by DMA
+    (FESOM2_P1V_UNION, MeshPlanDev::cu_ptr) -- the cluster bound read from the union's slots -- with
+    and without the large-partition rules (row pairs, stash, internal edges), odd and even L, variable
+    depth, a scattered numbering and Delaunay meshes (degrees 3..13: ring slices past the inline 8),
+    1 and 3 tracers; mode 2 puts the union's images in tvert's LDS region; a cap on the union's size
+    (FESOM2_P1V_UNION_MAX; 1: the block's own columns only) leaves the rest to memory gathers; every
+    output exact."""
+    from fesom2_amd import engine, synth
+    monkeypatch.setenv("FESOM2_P1V_UNION", mode)
+    if cap:
+        monkeypatch.setenv("FESOM2_P1V_UNION_MAX", cap)
+    if large:
+        monkeypatch.setenv("FESOM2_LARGE_CELLS", "0")
+    if name == "delaunay":
+        m = synth.delaunay_mesh(3000, nl, full_depth=nl == 48)
+    else:
+        g = synth.make_mesh(96, 40, nl, full_depth=nl == 48)
+        m = synth.permute_mesh(g) if name == "permuted" else g
+    tracers = synth.make_tracer_fields(m, ntr)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers) if ntr > 1 else engine.FctAle(dm, tracers[0])
+    try:
+        dm.prepare()
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        keys = ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")
+        got = {k: e.download(k).reshape(ntr, -1) for k in keys}
+        for k in range(ntr):
+            check_pass(m, {n: got[n][k] for n in keys}, O.full_pass(m, tracers[k]))
+    finally:
+        e.free()
+        dm.free()
+
+
+@pytest.mark.parametrize("group", ["2", "3"])
+@pytest.mark.parametrize("large", [True, False])
+@pytest.mark.parametrize("nl", [21, 48])
+def test_tracer_group_tile_order_matches_oracle(group, large, nl, monkeypatch):
+    """Round 6: batched tiles in groups of g tracers (FESOM2_TRACER_GROUP: every
+    column group of tracers 0..g-1, then the next g) for the tracer-fastest kernels; 6 tracers, with
+    and without the large-partition rules, split pass, every output exact."""
+    from fesom2_amd import engine, synth
+    monkeypatch.setenv("FESOM2_TRACER_GROUP", group)
+    if large:
+        monkeypatch.setenv("FESOM2_LARGE_CELLS", "0")
+    m = synth.make_mesh(96, 40, nl, full_depth=nl == 48)
+    tracers = synth.make_tracer_fields(m, 6)
+    dm = engine.DeviceMesh(m)
+    e = engine.FctAleBatch(dm, tracers)
+    try:
+        assert e.pre_comm_v() == 7, abi.last_error()
+        assert e.post_comm_h() == 9, abi.last_error()
+        e.sync()
+        keys = ("plus", "minus", "del_v", "del_h", "adf_v", "adf_h")
+        got = {k: e.download(k).reshape(6, -1) for k in keys}
+        for k in range(6):
+            check_pass(m, {n: got[n][k] for n in keys}, O.full_pass(m, tracers[k]))
+    finally:
+        e.free()
+        dm.free()

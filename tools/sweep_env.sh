@@ -3,11 +3,11 @@
 # Runs every configuration ROUNDS times, interleaved (A B C A B C ...), because the GPU's clocks
 # drift over minutes of back-to-back runs; one line per run in gpurun_out/sweep.txt.
 # A configuration may carry bench arguments after " | " ("FESOM2_X=1 | --path split").
-# BENCH_ARGS (eval'ed: may quote), STEPS, ROUNDS.
+# BENCH_ARGS (eval'ed: may quote), STEPS, ROUNDS, SWEEP_OUT (default gpurun_out/sweep.txt).
 set -o pipefail
 # the knobs exist in the tuning build only (make -C fesom2-accelerate_amd tuning)
 export FESOM2_LIB_NAME=${FESOM2_LIB_NAME:-libfesom2-accelerate-tuning.so}
-out=gpurun_out/sweep.txt
+out=${SWEEP_OUT:-gpurun_out/sweep.txt}
 : > $out
 for r in $(seq 1 ${ROUNDS:-1}); do
   for cfg in "$@"; do
