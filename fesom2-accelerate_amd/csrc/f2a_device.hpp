@@ -32,8 +32,7 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 //                   Infinity Cache); the product takes the direction per call (Tracers::order)
 //   c_tracer_group  FESOM2_TRACER_GROUP = g (batched tracers, tracer-fastest kernels): tiles run in
 //                   groups of g tracers -- every column group for tracers 0..g-1, then g..2g-1 -- so a
-//                   column's reuse by the next patch row comes g, not ntracers, tiles later per column;
-//                   overrides the per-call Tracers::group (0: the call's)
+//                   column's reuse by the next patch row comes g, not ntracers, tiles later per column
 #if F2A_TUNING
 static __constant__ int c_xcd_swizzle = 1;
 static __constant__ int c_ablate = 0;
@@ -162,9 +161,9 @@ __device__ __forceinline__ int block_tile() { return xcd_tile(blockIdx.x, gridDi
 // tile -> (column group, tracer): tracer fastest (the ntr blocks of a group share the XCD's L2
 // for the records and the mesh fields) or, with `major`, tracer slowest (each tracer's gathers
 // keep the L2 to themselves)
-// (gsz > 1: tiles in groups of gsz tracers -- Tracers::group -- every column group of tracers
-// 0..gsz-1 first, then the next gsz; the tuning build's FESOM2_TRACER_GROUP overrides it)
-__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false, bool rev = false, int gsz = 0)
+// (tuning: FESOM2_TRACER_GROUP = g > 1 tiles g tracers at a time -- every column group of tracers
+// 0..g-1 first, then the next g; measured neutral at 6 x 127k x 47 and 6 x 1.2M x 80)
+__device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false, bool rev = false)
 {
     const int t = rev ? xcd_tile_rev(blockIdx.x, gridDim.x) : block_tile();
     if (ntr == 1) {
@@ -176,7 +175,7 @@ __device__ __forceinline__ int group_tracer(int ntr, int &tr, bool major = false
         tr = t / groups;
         return t - tr * groups;
     }
-    const int gs = c_tracer_group ? c_tracer_group : gsz;
+    const int gs = c_tracer_group;
     if (gs > 1 && gs < ntr && ntr % gs == 0) {
         const int span = gridDim.x / ntr * gs;  // tiles of one tracer group
         const int tg = t / span, rem = t - tg * span, g = rem / gs;

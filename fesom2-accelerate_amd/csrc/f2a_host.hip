@@ -586,12 +586,6 @@ static bool build_b3h_pack(Plan *plan, MeshPlanDev &d, const std::vector<int4> &
     return desc.empty() || (d.b3p_desc && d.b3p_off);
 }
 
-int tracer_group(const Plan &plan, int ntr)
-{
-    if (plan.dev.cu_G <= 0 || ntr < 4) return 0;
-    return ntr % 3 == 0 ? 3 : ntr % 2 == 0 ? 2 : 0;
-}
-
 int pass_order(const Plan &plan, int ntr)
 {
     const MeshPlanDev &d = plan.dev;
@@ -795,9 +789,9 @@ ResolvedShape resolve_shape(const PlanShape &shape, long long wet_cells, int nl)
     r.strip = shape.strip == PlanShape::kAuto ? 0 : std::max(0, shape.strip);
     // cluster unions (MeshPlanDev::cu_ptr) in row-pair blocks on small partitions: p1v stages each
     // block's union of cluster columns into LDS once instead of gathering every column's cluster.
-    // Measured at 127k x 47 (24 level pairs): 6 tracers -11 % per pass with the tracer groups
-    // (tracer_group), 1 tracer -3 to -7 %; at 1.2M x 80 (large partitions) +9 to +50 % -- the LDS
-    // images cost occupancy there.  The cap keeps the images to 16 KB per block (21 columns at L =
+    // Measured at 127k x 47 (24 level pairs; one set of buffers, interleaved): 6 tracers -2.3 to
+    // -3.1 % per pass (p1v -4.4 %), 1 tracer -1.2 %; at 1.2M x 80 (large partitions) +9 to +50 % --
+    // the LDS images cost occupancy there.  The cap keeps the images to 16 KB per block (21 columns at L =
     // 47: the 4 x 2 blocks' unions hold 22, the last one gathered from memory).  Plan option
     // FESOM2_P1V_UNION: 0 off, unset automatic (small partitions, L <= 64), > 0 on (the tuning
     // build: 1 or 2 also picks the kernel's LDS layout)
@@ -972,6 +966,10 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
         // tuning build
         const int porder = knob("FESOM2_PATCH_ORDER", local_numbering ? 0 : 1);
         std::vector<int> order;
+        // a union plan's row pairs serve p1v's blocks only: b3h's edge order and phase 2's node
+        // records follow the patches' plain order (`plain`), which streams better for them (127k x 47:
+        // row pairs cost b3h 2 % and p2h 1 %)
+        std::vector<int> plain;
         std::vector<int> stamp, bq;  // FESOM2_PATCH_ORDER = 1: patch membership stamps, BFS queue
         if (porder == 1) stamp.assign(n_owned, -1);
         int npatch = 0;
@@ -1025,9 +1023,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
                     } else {
                         std::sort(cur.begin(), cur.end());
                     }
+                    if (rs.union_cap > 0) plain.insert(plain.end(), cur.begin(), cur.end());
                 } else {
                     std::sort(cur.begin(), cur.end());
                     if (rs.strip > 0) strip_order(cur, rs.strip, ptr, other);
+                    if (rs.union_cap > 0) plain.insert(plain.end(), cur.begin(), cur.end());
                     // row pairs on large partitions, with the stash below (1.2M x 80: -2.2 % with 6
                     // columns, 6 tracers -1.2 %)
                     // (tuning: FESOM2_ROWPAIR = R > 1 takes R rows per block)
@@ -1130,7 +1130,8 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             etaken[e] = 1;
             einfo.push_back(make_int4(m.edges[2 * (size_t)e] - 1, m.edges[2 * (size_t)e + 1] - 1, lev[e], e));
         };
-        for (int v : order)
+        if (plain.size() != order.size()) plain = order;  // (index order, or no union plan)
+        for (int v : plain)
             for (int k = ptr[v]; k < ptr[v + 1]; k++)
                 if (!etaken[refs[k].edge]) push_edge(refs[k].edge);
         for (int e = 0; e < n_edges; e++)
@@ -1234,6 +1235,11 @@ std::unique_ptr<Plan> build_plan(const HostMesh &m, int n_owned, int n_total, in
             for (int k = ptr[n]; k < ptr[n + 1]; k++)
                 if (other[k] >= n_owned) interior_node[n] = 0;
         std::vector<NodeRec> p2(recs);
+        if (plain != order) {  // phase 2 in the plain order (see `plain`)
+            std::vector<int> at(n_owned);
+            for (int k = 0; k < n_owned; k++) at[order[k]] = k;
+            for (int k = 0; k < n_owned; k++) p2[k] = recs[at[plain[k]]];
+        }
         std::stable_partition(p2.begin(), p2.end(), [&](const NodeRec &r) { return interior_node[r.info.n] != 0; });
         d.n_p2_interior = (int)std::count(interior_node.begin(), interior_node.end(), (char)1);
         for (int n = 0; n < n_owned; n++) d.max_degree = std::max(d.max_degree, ptr[n + 1] - ptr[n]);

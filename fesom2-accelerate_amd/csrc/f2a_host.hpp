@@ -200,10 +200,6 @@ struct Plan {
 // every kernel forwards with non-temporal flux stores (measured).
 constexpr long long kCacheOrderBytes = 192ll << 20;
 int pass_order(const Plan &plan, int ntr);
-// Tracers::group of a batched call of `ntr` tracers on `plan`: on a plan with cluster unions (small
-// partitions) the tracer-fastest kernels tile 3 (or 2) tracers at a time -- measured with the unions
-// at 6 x 127k x 47 -- else every tracer interleaved (0)
-int tracer_group(const Plan &plan, int ntr);
 
 // Processing-order options of a plan.  Single-tracer calls use the defaults (16384-node patches
 // for a numbering with locality, the natural block size); calls with ntracers > 1 get a plan of

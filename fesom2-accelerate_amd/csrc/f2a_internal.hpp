@@ -193,9 +193,6 @@ struct Tracers {
     // pass order (pass_order, f2a_host.hpp): bit 0 the p1 kernels and bit 2 the p2 node kernels
     // walk each XCD's tile range backwards, bit 3 b3h stores the limited fluxes cache-allocating
     int order = 0;
-    // tracer-fastest kernels (p1, p2h): tiles in groups of `group` tracers (0: all interleaved),
-    // see tracer_group (f2a_host.hpp)
-    int group = 0;
 };
 
 // Kernel launchers (fct_ale_kernels.hip).  All enqueue on `s` and return hipGetLastError().

@@ -326,7 +326,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     const int L = a0.nl - 1, S = (L + C - 1) / C;  // ODD: pairs, the last slot holds one level
     const int t = threadIdx.x;
     int tr = 0;
-    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, (c_tile_rev | a0.tr.order) & 1, a0.tr.group);
+    const int grp = group_tracer(a0.tr.n, tr, c_tracer_major & 1, (c_tile_rev | a0.tr.order) & 1);
     const int first = grp * G;
     const int ncol = min(G, a0.n_owned - first);
     // doubles in front of the records: tvert max | min, or (OPT & 1024) the larger of that and the
@@ -757,7 +757,7 @@ __global__ __launch_bounds__(1024) void k_p2h(MeshPlanDev mp, P2Args a, int G, f
     extern __shared__ real lds[];  // NodeRec[G]
     const int L = a.nl - 1, S = (L + C - 1) / C;
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4, a.tr.group) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
     if (tr) {
         a.del_h += tr * a.tr.node;
         a.adf_h += tr * a.tr.edge;
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(1024) void k_p2(MeshPlanDev mp, P2Args a, int G, fl
 {
     extern __shared__ real lds[];  // NodeRec[G]
     int tr;
-    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4, a.tr.group) * G;
+    const int first = group_tracer(a.tr.n, tr, c_tracer_major & 4, (c_tile_rev | a.tr.order) & 4) * G;
     if (tr) {
         a.plus += tr * a.tr.node;
         a.minus += tr * a.tr.node;

@@ -397,7 +397,6 @@ static void pre_comm_fused_impl(int *alg_state, void **s, int *ntracers, void **
                   *dt, *flux_eps, *bignumber};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
     a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
-    a.tr.group = f2a::tracer_group(*plan, ntr);  // tracer groups of the tracer-fastest kernels
     if (vertical) {
         a.area = dptr<real>(barea);
         a.hnode = dptr<real>(bh);
@@ -678,7 +677,6 @@ static void post_comm_c_impl(int *alg_state, void **s, void **fct_plus, void **f
                   dptr<real>(bdv), dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
     a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
-    a.tr.group = f2a::tracer_group(*plan, ntr);  // tracer groups of the tracer-fastest kernels
     // b3-horizontal as its own edge kernel, then the node kernel (the alternatives measured slower:
     // DESIGN.md §3)
     {
@@ -764,7 +762,6 @@ void fct_ale_post_comm_h_acc_(int *alg_state, void **s, int *ntracers, void **co
                   dptr<real>(barea), nullptr, dptr<real>(badfh), nullptr, dptr<real>(bdh), *dt};
     a.tr = f2a::Tracers{ntr, (size_t)NT * L, (size_t)NT * NL, (size_t)E * L};
     a.tr.order = f2a::pass_order(*plan, ntr);  // kernel directions (Infinity Cache reuse)
-    a.tr.group = f2a::tracer_group(*plan, ntr);  // tracer groups of the tracer-fastest kernels
     const f2a::MeshPlanDev &de = ip ? ip->dev : d;  // the edge lists b3h runs on
     const int eb = de.n_edge_interior;               // boundary edges (a halo endpoint): [eb, E)
     if (!run("fct_ale_b3_horizontal", st, [&] {

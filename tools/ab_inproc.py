@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""In-process interleaved A/B of tuning-build variants: one mesh, one engine and plan per variant,
-the variants' passes alternating in short bursts inside ONE process, so clock and thermal drift
-(which moves separate bench.py runs by up to 7 % on some boxes) hits every variant alike.
+"""In-process interleaved A/B of tuning-build variants: one mesh, one set of field buffers, one set
+of mesh handles and plans per variant, the variants' passes alternating in short bursts inside ONE
+process, so clock and thermal drift (which moves separate bench.py runs by up to 7 % on some boxes)
+hits every variant alike.
 
 Each variant is a set of FESOM2_* knobs (tuning build, FESOM2_LIB_NAME): they are set while the
 variant's plans are built (fesom2_prepare_mesh_) and again around each of its bursts (the launch-time
@@ -62,22 +63,28 @@ def main():
     abi.set_resident(True)
     m = synth.config_mesh(a.config, full_depth=not a.parity_levels)  # as bench.py builds it
     tracers = synth.make_tracer_fields(m, a.tracers)
-    runs = []
+    # ONE set of field buffers for every variant (separate allocations differ by up to 6 % in what
+    # they stream -- measured with duplicate variants): each variant has its own mesh handles, hence
+    # its own plans (cached by handle identity), and the engine is pointed at them in turn
+    runs, e = [], None
     for name, env in variants:
         with Knobs(env, keys):
             dm = engine.DeviceMesh(m)
             dm.prepare()
-            e = engine.FctAleBatch(dm, tracers) if a.tracers > 1 else engine.FctAle(dm, tracers[0])
+            if e is None:
+                e = engine.FctAleBatch(dm, tracers) if a.tracers > 1 else engine.FctAle(dm, tracers[0])
+                e.drop_host()  # resident: the library never reads them again (large meshes: host memory)
+            e.dm = dm
             for _ in range(3):  # warmup (and the plan, should prepare have missed it)
                 assert e.split_pass() == 9, abi.last_error()
             e.sync()
-            e.drop_host()  # resident: the library never reads them again (large meshes: host memory)
         runs.append((name, env, dm, e))
     del tracers
     times = {name: [] for name, *_ in runs}
     for r in range(a.rounds):
         order = runs if r % 2 == 0 else runs[::-1]
         for name, env, dm, e in order:
+            e.dm = dm
             with Knobs(env, keys):
                 abi.device_sync()
                 t0 = time.perf_counter()
@@ -87,6 +94,7 @@ def main():
                 times[name].append(1e3 * (time.perf_counter() - t0) / a.burst)
     kernels = {}
     for name, env, dm, e in runs:
+        e.dm = dm
         with Knobs(env, keys):
             abi.kernel_timing(True)
             abi.kernel_timing_reset()
@@ -103,8 +111,8 @@ def main():
                                  "vs_first": round(med / base - 1, 4), "kernels_ms": kernels[name]}
         print(f"{name:28s} {med:8.4f} ms  ({100 * (med / base - 1):+.1f} %)  {kernels[name]}", flush=True)
     print(json.dumps(out))
-    for name, env, dm, e in runs:
-        e.free()
+    e.free()
+    for name, env, dm, _ in runs:
         dm.free()
 
 
