@@ -7,6 +7,7 @@
 # usage (on the GPU box): bash tools/mem_breakdown.sh TAG ['name|bench args' ...]  -> gpurun_out/mem_TAG/...
 #   default workloads: 1p2M (the headline) and 6tr (--tracers 6); e.g. the 127k x 47 pair:
 #   bash tools/mem_breakdown.sh r06 "127k|--config '127k x 47'" "127k6|--config '127k x 47' --tracers 6"
+#   (a third field sets environment variables for that workload: "off|--tracers 6|FESOM2_P1V_UNION=0")
 set -eo pipefail
 tag=${1:-r05}
 shift || true
@@ -21,20 +22,23 @@ A=$(have TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCES
 B=$(have TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_TAG_STALL_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_UTCL1_TRANSLATION_MISS_sum TD_TD_BUSY_sum TD_TC_STALL_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TOTAL_WAVEFRONTS_sum)
 C=$(have TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_sum)
 { echo "pass A: $A"; echo "pass B: $B"; echo "pass C: $C"; } > "$out/passes.txt"
-run() {  # workload pass counters... -- bench args...
+run() {  # workload pass counters... -- bench args...   (WL_ENV: K=V ... for this workload)
     local wl=$1 ps=$2; shift 2
     local ctr=()
     while [ "$1" != "--" ]; do ctr+=("$1"); shift; done
     shift
-    timeout -k 10 -s KILL 180 rocprofv3 --pmc "${ctr[@]}" --output-format csv -d "$out/${wl}_$ps" -o pmc -- \
+    env ${WL_ENV:-} timeout -k 10 -s KILL 180 rocprofv3 --pmc "${ctr[@]}" --output-format csv -d "$out/${wl}_$ps" -o pmc -- \
         python3 bench.py --no-cpu-baseline --no-check --extras none --steps 3 --warmup 1 "$@" \
         > "$out/${wl}_$ps.json" 2> "$out/${wl}_$ps.err"
 }
 for ps in A B C; do
     eval "ctr=\$$ps"
     for w in "${wls[@]}"; do
-        eval "wargs=(${w#*|})"
-        run "${w%%|*}" $ps $ctr -- "${wargs[@]}"
+        rest=${w#*|}
+        WL_ENV=""
+        if [[ "$rest" == *"|"* ]]; then WL_ENV=${rest#*|}; rest=${rest%%|*}; fi  # name|args|K=V K=V
+        eval "wargs=($rest)"
+        WL_ENV="$WL_ENV" run "${w%%|*}" $ps $ctr -- "${wargs[@]}"
     done
 done
 find "$out" -name "*.csv" | sort > "$out/files.txt"
