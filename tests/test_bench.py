@@ -383,7 +383,8 @@ def test_traffic_is_reported_only_for_the_library_it_measured(tmp_path):
     # the emulated rank: only a file stamped with its rank/world
     e = argparse.Namespace(**dict(vars(a), config="9.6M x 80", scaling="strong", emulate=(3, 8)))
     path.write_text(json.dumps(dict(doc, workload="9.6M x 80")))
-    assert bench.find_traffic(e, 1, "fct_ale_p1v") == (None, {})
+    mine = os.path.relpath(str(path), bench.ROOT)
+    assert bench.find_traffic(e, 1, "fct_ale_p1v")[1].get("traffic_source") != mine  # (the repo's own rank file may)
     path.write_text(json.dumps(dict(doc, workload="9.6M x 80", emulate="3/8")))
     assert bench.find_traffic(e, 1, "fct_ale_p1v")[0] == 123
     assert bench.traffic_paths(e)[-1].endswith("traffic_9p6Mx80_rank3of8.json")
