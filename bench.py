@@ -855,6 +855,9 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
     dm.prepare()
     mi = dm.info(batched=args.tracers > 1 and mode != "producer")
     mesh_info = {"ice": mi["internal_edge_cells"], "nie": mi["internal_edges"]}
+    # the plan the kernels ran on: p1v block columns, block-internal edges, cluster unions
+    plan_info = {"p1v_columns": mi["p1v_columns"], "internal_edges": mi["internal_edges"],
+                 "union_columns": mi.get("union_columns", 0), "union_max": mi.get("union_max", 0)}
     order = dm.pass_order(args.tracers if mode != "producer" else 1)  # the Infinity-Cache pass order
     if args.fct_iter > 1 and (world > 1 or args.tracers > 1 or mode):
         raise SystemExit("--fct-iter: 1 GPU, 1 tracer, device resident")
@@ -1190,7 +1193,7 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
            "pass_roofline": pr,
            "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
            "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s,
-           "pass_order": order}
+           "pass_order": order, "plan": plan_info}
     if world > 1:
         ms = [r[0] for r in per_rank]
         rec["ranks"] = {
@@ -1303,7 +1306,7 @@ def compact(rec, args, world):
            "nodes_per_gpu": m.N, "levels": m.L, "cells_per_gpu": s["cn"], "tracers": args.tracers,
            "roofline": rec["roofline"], "pass_roofline": rec["pass_roofline"],
            "kernels_ms": {k: v["avg_ms"] for k, v in rec["kernels"].items()}, "check": rec["check"],
-           "setup_s": rec["setup_s"], "pass_order": rec["pass_order"]}
+           "setup_s": rec["setup_s"], "pass_order": rec["pass_order"], "plan": rec.get("plan")}
     for k in ("ranks", "rccl_nranks", "transfers"):
         if k in rec:
             out[k] = rec[k]
@@ -1481,6 +1484,7 @@ def main():
                      "device resident (inputs in HBM before the timed region)",
         "setup_s": head["setup_s"],
         "pass_order": head["pass_order"],
+        "plan": head.get("plan"),
     }
     if head["check"] is not None:
         out["check"] = head["check"]

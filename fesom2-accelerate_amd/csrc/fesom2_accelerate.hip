@@ -1039,13 +1039,17 @@ void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim
     mh.nie_num = buf(nod_in_elem2D_num, "nod_in_elem2D_num");
     mh.dim = *nod_in_elem2D_dim;
     if (!mh.edges || !mh.edge_tri || !mh.nlev_elem || !mh.nlev_nod || !mh.elem_nodes || !mh.nie || !mh.nie_num) return;
-    const int n = std::min(*ninfo, 10);
-    for (int part = 0; part * 5 < n; part++) {  // [0, 5) the single-tracer plan, [5, 10) the batched one
+    const int n = std::min(*ninfo, 14);
+    for (int part = 0; part < 2; part++) {  // [0, 5) the single-tracer plan, [5, 10) the batched one
+        if (part * 5 >= n) break;
         const Plan *plan = get_plan(mh, N, NT, E, *nl, true, part == 1);
         if (!plan) return;
         const long long v[5] = {plan->dev.int_G, plan->dev.n_edge_interior, plan->dev.n_ext_interior,
                                 plan->dev.n_edge_interior - plan->dev.n_ext_interior, plan->int_cells};
         for (int k = 0; k < 5 && part * 5 + k < n; k++) info[part * 5 + k] = v[k];
+        // [10, 12) / [12, 14): the plan's cluster unions -- p1v block columns (0 = none), largest union
+        const long long u[2] = {plan->dev.cu_G, plan->dev.cu_max};
+        for (int k = 0; k < 2 && 10 + 2 * part + k < n; k++) info[10 + 2 * part + k] = u[k];
     }
     *ninfo = n;
     *istat = 0;

@@ -58,15 +58,18 @@ class DeviceMesh:
         block-internal ones (limited inside p1v) and their edge cells -- of the single-tracer plan,
         or with ``batched`` of the plan calls with ntracers > 1 run on."""
         m, h = self.m, self.h
-        st, n = C.c_int(0), C.c_int(10 if batched else 5)
-        out = (C.c_longlong * 10)()
+        st, n = C.c_int(0), C.c_int(14)
+        out = (C.c_longlong * 14)()
         dll().fesom2_mesh_info_(C.byref(st), ip(m.N), ip(m.H), ip(m.T), ip(m.E), ip(m.nl), h["nlev_nod"].ref,
                                 h["nlev_elem"].ref, h["elem2D_nodes"].ref, h["nie_num"].ref, h["nie"].ref,
                                 ip(m.dim), h["edges"].ref, h["edge_tri"].ref, out, C.byref(n))
         check(st, "fesom2_mesh_info_")
         keys = ("p1v_columns", "interior_edges", "crossing_edges", "internal_edges", "internal_edge_cells")
         vals = list(out)[: n.value]
-        return dict(zip(keys, vals[5:] if batched else vals))
+        d = dict(zip(keys, vals[5:10] if batched else vals[:5]))
+        if n.value >= 14:  # the cluster unions (0 columns: none)
+            d["union_columns"], d["union_max"] = vals[12:14] if batched else vals[10:12]
+        return d
 
     def pass_order(self, ntracers=1):
         """fesom2_pass_order_: the Infinity-Cache pass order of a call of ``ntracers`` tracers

@@ -155,8 +155,9 @@ void fesom2_prepare_mesh_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *my
 /* Diagnostics of the phase-1 mesh plan (built if needed): info[0] p1v block columns of the
  * block-internal edge lists (0 = none), [1] interior edges, [2] interior edges crossing p1v blocks,
  * [3] block-internal edges (limited inside fct_ale_pre_comm_v_acc_), [4] their edge cells;
- * [5, 10) the same for the plan of batched calls (ntracers > 1).  *ninfo: capacity in (at most 10
- * used), entries written out. */
+ * [5, 10) the same for the plan of batched calls (ntracers > 1); [10], [11] the single-tracer plan's
+ * cluster unions (p1v block columns, 0 = none; the largest union), [12], [13] the batched plan's.
+ * *ninfo: capacity in (at most 14 used), entries written out. */
 void fesom2_mesh_info_(int *istat, int *myDim_nod2D, int *eDim_nod2D, int *myDim_elem2D, int *myDim_edge2D,
                        int *nl, void **nlevels_nod2D, void **nlevels_elem2D, void **elem2D_nodes,
                        void **nod_in_elem2D_num, void **nod_in_elem2D, int *nod_in_elem2D_dim,

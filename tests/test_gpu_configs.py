@@ -67,6 +67,7 @@ def test_config2_split_pass_1p2m_x_80_automatic_plan(monkeypatch):
         dm.prepare()
         info = dm.info()
         assert info["internal_edges"] > 0.2 * m.E, info  # automatic: block-internal edges in p1v
+        assert info["union_columns"] == 0, info  # large partition: no cluster unions
         e = engine.FctAle(dm, f, copy=False)
         assert e.split_pass() == 9, abi.last_error()
         e.sync()
@@ -87,6 +88,11 @@ def test_config3_batched_split_pass(name, ntr):
     dm = engine.DeviceMesh(m)
     e = engine.FctAleBatch(dm, tracers)
     try:
+        info = dm.info(batched=True)
+        if name == "127k x 47":  # small partition: cluster unions of 8-column row-pair blocks, capped
+            assert info["union_columns"] == 8 and 8 < info["union_max"] <= 21, info
+        else:
+            assert info["union_columns"] == 0, info
         assert e.split_pass() == 9, abi.last_error()
         e.sync()
         got = {k: e.download(k).reshape(ntr, -1) for k in FIELDS}
