@@ -63,25 +63,22 @@ __device__ __forceinline__ int xcd_tile_rev(int b, int G)
     return x * q + (x < r ? x : r) + (len - 1 - k);
 }
 
-// the tuning build's knobs of the __constant__ switches above (the product keeps the defaults)
+// the tuning build's knobs of the __constant__ switches above (the product keeps the defaults), read
+// at every launch and copied to the device when they change -- so an in-process A/B
+// (tools/ab_inproc.py) can switch them between bursts
 static void init_swizzle()
 {
 #if F2A_TUNING
-    static bool done = false;
-    if (done) return;
-    done = true;
-    if (knob("FESOM2_XCD", 1) == 0) {
-        const int zero = 0;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_xcd_swizzle), &zero, sizeof zero);
-    }
-    if (const int v = knob("FESOM2_TRACER_MAJOR", -1); v >= 0)
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_major), &v, sizeof v);
-    if (const int v = knob("FESOM2_ABLATE", 0); v != 0)
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ablate), &v, sizeof v);
-    if (const int v = knob("FESOM2_TILE_REV", 0); v != 0)
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tile_rev), &v, sizeof v);
-    if (const int v = knob("FESOM2_TRACER_GROUP", 0); v != 0)
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tracer_group), &v, sizeof v);
+    static int last[5] = {1, 2, 0, 0, 0};  // the __constant__ initialisers
+    const int v[5] = {knob("FESOM2_XCD", 1) == 0 ? 0 : 1, knob("FESOM2_TRACER_MAJOR", 2), knob("FESOM2_ABLATE", 0),
+                      knob("FESOM2_TILE_REV", 0), knob("FESOM2_TRACER_GROUP", 0)};
+    const void *sym[5] = {(const void *)&c_xcd_swizzle, (const void *)&c_tracer_major, (const void *)&c_ablate,
+                          (const void *)&c_tile_rev, (const void *)&c_tracer_group};
+    for (int k = 0; k < 5; k++)
+        if (v[k] != last[k]) {
+            (void)hipMemcpyToSymbol(sym[k], &v[k], sizeof v[k]);
+            last[k] = v[k];
+        }
 #endif
 }
 
