@@ -517,7 +517,11 @@ def test_degenerate_level_counts(kind, mode, monkeypatch):
 # plan options of the product library (read once when a mesh plan is built)
 PLAN_OPTIONS = [{"FESOM2_P1V_B3H": "0"}, {"FESOM2_P1V_B3H": "1"}, {"FESOM2_PATCH": "64"}, {"FESOM2_PATCH": "0"},
                 {"FESOM2_PATCH": "100", "FESOM2_P1V_B3H": "1"}, {"FESOM2_PATCH": "4096", "FESOM2_P1V_B3H": "1"},
-                {"FESOM2_CACHE_ORDER": "0"}, {"FESOM2_CACHE_ORDER": "1", "FESOM2_P1V_B3H": "1"}]
+                {"FESOM2_CACHE_ORDER": "0"}, {"FESOM2_CACHE_ORDER": "1", "FESOM2_P1V_B3H": "1"},
+                # round 6: cluster unions off (the plain gather plan) / forced on with the large-partition
+                # rules (row-pair blocks of 6 at L = 80, internal edges, stash) / with a patch size
+                {"FESOM2_P1V_UNION": "0"}, {"FESOM2_P1V_UNION": "1", "FESOM2_LARGE_CELLS": "0"},
+                {"FESOM2_P1V_UNION": "1", "FESOM2_PATCH": "100"}]
 
 
 @pytest.mark.parametrize("nl", [3, 4, 5, 48, 81, 129])
