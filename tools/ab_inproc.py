@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--config", default="127k x 47")
     ap.add_argument("--tracers", type=int, default=1)
     ap.add_argument("--parity-levels", action="store_true", help="variable depth (bench.py's flag); default full depth")
+    ap.add_argument("--mesh", default="structured", choices=["structured", "delaunay", "delaunay-hilbert"],
+                    help="as bench.py: Delaunay triangulation of as many random points as the config has nodes")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--burst", type=int, default=20)
     ap.add_argument("variants", nargs="+")
@@ -61,7 +63,12 @@ def main():
     keys = sorted({k for _, env in variants for k in env})
     abi.set_mpi_rank(0, 1)
     abi.set_resident(True)
-    m = synth.config_mesh(a.config, full_depth=not a.parity_levels)  # as bench.py builds it
+    if a.mesh == "structured":
+        m = synth.config_mesh(a.config, full_depth=not a.parity_levels)  # as bench.py builds it
+    else:
+        nx, ny, nl = synth.CONFIGS[a.config]
+        m = synth.delaunay_mesh(nx * ny, nl, full_depth=not a.parity_levels,
+                                numbering="hilbert" if a.mesh == "delaunay-hilbert" else "scipy")
     tracers = synth.make_tracer_fields(m, a.tracers)
     # ONE set of field buffers for every variant (separate allocations differ by up to 6 % in what
     # they stream -- measured with duplicate variants): each variant has its own mesh handles, hence
