@@ -329,6 +329,68 @@ def test_partitioned_pass_on_one_gpu(kind, nranks):
     assert_cols_equal(owned_plus, want["plus"], g.nlev_nod, g.L, g.N, "plus")
 
 
+@pytest.mark.parametrize("ntr", [1, 3])
+@pytest.mark.parametrize("kind", ["strips", "random", "delaunay"])
+def test_partitioned_split_pass_with_cluster_unions(kind, ntr):
+    """The default entry sequence on halo meshes at FESOM2's per-GPU depth class (nl - 1 <= 64, so
+    the plans stage p1v's cluster unions in LDS, and the unions hold halo columns):
+    fct_ale_pre_comm_v_acc_ per partition, the caller's exchange of fct_plus/fct_minus on the host,
+    fct_ale_post_comm_h_acc_; 1 tracer and a batch of 3.  Owned results equal the single-domain
+    oracle exactly."""
+    from fesom2_amd import partition
+    nl, nranks = 21, 3
+    if kind == "delaunay":
+        g = synth.delaunay_mesh(4000, nl)
+        part = np.random.default_rng(11).integers(0, nranks, g.N).astype(np.int32)
+    else:
+        nx, ny = 64, 48
+        g = synth.make_mesh(nx, ny, nl)
+        part = (partition.strip_parts(nx, ny, nranks) if kind == "strips"
+                else np.random.default_rng(3).integers(0, nranks, g.N).astype(np.int32))
+    gtr = synth.make_tracer_fields(g, ntr)
+    want = [O.full_pass(g, gtr[k]) for k in range(ntr)]
+    locs = [partition.local_mesh(g, part, r) for r in range(nranks)]
+    runs = []
+    try:
+        for m, _ in locs:
+            dm = engine.DeviceMesh(m)
+            assert dm.info(batched=ntr > 1)["union_columns"] > 0
+            ftr = synth.make_tracer_fields(m, ntr)
+            runs.append((dm, engine.FctAle(dm, ftr[0]) if ntr == 1 else engine.FctAleBatch(dm, ftr)))
+        for _, e in runs:
+            assert e.pre_comm_v() == 7, abi.last_error()
+        pm = []
+        for _, e in runs:
+            e.sync()
+            pm.append([e.download(k).reshape(ntr, -1, g.L) for k in ("plus", "minus")])
+        for r, (m, h) in enumerate(locs):
+            for q in h.neighbors:
+                src, dst = locs[q][1].send[r] - 1, h.recv[q] - 1
+                for a in range(2):
+                    pm[r][a][:, dst] = pm[q][a][:, src]
+            for a, name in enumerate(("plus", "minus")):
+                runs[r][1].upload(name, pm[r][a].reshape(-1))
+        for _, e in runs:
+            assert e.post_comm_h() == 9, abi.last_error()
+        outs = []
+        for _, e in runs:
+            e.sync()
+            outs.append({k: e.download(k).reshape(ntr, -1) for k in ("del_v", "del_h", "adf_v")})
+    finally:
+        for dm, e in runs:
+            e.free()
+            dm.free()
+    ms = [m for m, _ in locs]
+    for t in range(ntr):
+        for k in ("del_v", "del_h"):
+            got = partition.gather_owned(ms, lambda r: outs[r][k][t], g.L, g.N)
+            assert np.array_equal(got, want[t][k]), (k, t)
+        got = partition.gather_owned(ms, lambda r: outs[r]["adf_v"][t], g.nl, g.N)
+        assert np.array_equal(got, want[t]["adf_v"]), ("adf_v", t)
+        owned_plus = partition.gather_owned(ms, lambda r: pm[r][0][t].reshape(-1), g.L, g.N)
+        assert_cols_equal(owned_plus, want[t]["plus"], g.nlev_nod, g.L, g.N, "plus")
+
+
 def test_reference_named_entries_run_on_gpu():
     """fct_ale_a1_reference_ .. fct_ale_pre_comm_ (reference .h:142, :225-235) on host arrays,
     executed by the HIP engine: same results as reference.cpp's CPU functions."""
