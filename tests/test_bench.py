@@ -388,3 +388,20 @@ def test_traffic_is_reported_only_for_the_library_it_measured(tmp_path):
     path.write_text(json.dumps(dict(doc, workload="9.6M x 80", emulate="3/8")))
     assert bench.find_traffic(e, 1, "fct_ale_p1v")[0] == 123
     assert bench.traffic_paths(e)[-1].endswith("traffic_9p6Mx80_rank3of8.json")
+
+
+def test_committed_traffic_files_match_the_built_library():
+    """Every profiles/traffic*.json is stamped with the code object of the library built from this
+    tree: a kernel change without a new PMC pass (tools/profile.sh, TRAFFIC_OUT) fails here instead
+    of leaving the round-end bench line with traffic_stale."""
+    import glob
+    import json
+    from fesom2_amd import _paths
+    try:
+        code = _paths.code_object_hash()
+    except (OSError, ValueError):
+        pytest.skip("engine library not built")
+    files = sorted(glob.glob(os.path.join(bench.ROOT, "profiles", "traffic*.json")))
+    assert files
+    stale = [os.path.basename(p) for p in files if json.load(open(p)).get("code_object") != code]
+    assert not stale, f"stamped with another build than {code}: {stale}"
