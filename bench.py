@@ -781,6 +781,50 @@ def oracle_halo_plus_minus(nx, ny, nl, full_depth, vlimit, world, rank):
     return plus, minus
 
 
+def single_pass_baseline(args, m, dm, batch_ms):
+    """A batched leg's tracers the way the reference takes them: one tracer per call
+    (`src/fesom2-accelerate.cu:258-379`), each its own buffers, their direction-split passes in
+    sequence on one stream -- warmup, then ``args.steps`` sequences, wall time between device syncs.
+    Distinct tracers: six repeats of ONE tracer would find the previous pass's tail in the Infinity
+    Cache, which a sequence of different tracers does not (profiles/r06/s23)."""
+    stream = abi.Stream()
+    engines, shared = [], None
+    try:
+        for k in range(args.tracers):
+            fk = synth.make_fields(m, seed=43 + k)  # the fields make_tracer_fields gives tracer k
+            if shared is None:
+                shared = {n: fk[n] for n in ("area", "area_inv", "hnode", "hnode_new")}
+            fk.update(shared)
+            e = engine.FctAle(dm, fk, stream=stream, vlimit=args.vlimit, copy=False)
+            e.drop_host()
+            engines.append(e)
+            del fk
+
+        def sequence():
+            for e in engines:
+                s1 = e.pre_comm_v()
+                s2 = e.post_comm_h() if s1 == 7 else s1
+                if s2 != 9:
+                    raise RuntimeError(f"single-tracer pass alg_state {s2}: {abi.last_error()}")
+
+        for _ in range(max(1, args.warmup)):
+            sequence()
+        abi.device_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sequence()
+        abi.device_sync()
+        ms = 1e3 * (time.perf_counter() - t0) / args.steps
+    finally:
+        for e in engines:
+            e.free()
+        stream.free()
+    return {"ms_per_step": round(ms, 4), "batch_gain": round(batch_ms / ms - 1, 4),
+            "note": f"the same {args.tracers} tracers as single-tracer split passes (pre_comm_v -> post_comm_h) in "
+                    f"sequence, each tracer its own buffers, one stream, {args.steps} sequences after "
+                    f"{max(1, args.warmup)} of warmup; batch_gain = batch ms / this - 1"}
+
+
 # ----------------------------------------------------------------------------- one leg
 
 class Ctx:
@@ -1181,6 +1225,13 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
         log(f"check ({args.leg}): {check}")
     if graph is not None:
         graph.free()
+    # the same tracers as the reference calls them, one tracer per call in sequence (batched
+    # device-resident legs on one GPU; after the timed region and the check)
+    singles = None
+    if args.tracers > 1 and not mode and world == 1 and not em and args.fct_iter == 1 and args.path == "split" \
+            and not args.graph and not getattr(args, "no_single_baseline", False):
+        singles = single_pass_baseline(args, m, dm, ms_step)
+        log(f"single-tracer passes ({args.leg}): {singles}")
 
     # the whole pass's figures also inside `roofline` (the driver's parsed record keeps that object
     # whole; pass_roofline stays beside it): frac of 8 TB/s and of this run's copy rate
@@ -1194,6 +1245,8 @@ def run_leg(args, ctx, headline=False, cpu_all=None, ceiling=None):
            "kernels": per_kernel, "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
            "setup_s": round(setup_s, 1), "cpu": cpu, "check": check, "m": m, "s": s,
            "pass_order": order, "plan": plan_info}
+    if singles:
+        rec["single_passes"] = singles
     if world > 1:
         ms = [r[0] for r in per_rank]
         rec["ranks"] = {
@@ -1307,7 +1360,7 @@ def compact(rec, args, world):
            "roofline": rec["roofline"], "pass_roofline": rec["pass_roofline"],
            "kernels_ms": {k: v["avg_ms"] for k, v in rec["kernels"].items()}, "check": rec["check"],
            "setup_s": rec["setup_s"], "pass_order": rec["pass_order"], "plan": rec.get("plan")}
-    for k in ("ranks", "rccl_nranks", "transfers"):
+    for k in ("ranks", "rccl_nranks", "transfers", "single_passes"):
         if k in rec:
             out[k] = rec[k]
     if getattr(args, "emulate", None):
@@ -1334,6 +1387,8 @@ def main():
     ap.add_argument("--permuted", action="store_true",
                     help="shuffle node/element/edge numbering (unstructured stress variant, 1 GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-baseline", action="store_true",
+                    help="batched legs: skip timing the same tracers as single-tracer passes in sequence")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle passes for cpu_baseline")
     ap.add_argument("--path", default="split", choices=["fused", "split", "stepwise", "reference", "reference-plain"],
                     help="fused: pre_comm + post_comm_c; split: pre_comm_v (+ b3v, cv) + post_comm_h (b3h, ch); "
