@@ -421,7 +421,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
     if constexpr ((OPT & 512) != 0) {
         // the union's LO and ttf columns global -> LDS, 16 B per lane: item f of [array][slot][pair]
         // lands at uLO + 2f, i.e. each wave's 64 items fill 1 KB of LDS (landed at the next barrier)
-        const int per = nU * S, items = 2 * per;
+        const int per = nU * S, items = (c_ablate & 32) ? 0 : 2 * per;
         for (int f0 = (t >> 6) * kWave; f0 < items; f0 += (int)blockDim.x) {
             const int f = f0 + (t & (kWave - 1));
             if (f < items) {
@@ -458,7 +458,7 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
             const f2a_d2u t = *reinterpret_cast<const f2a_d2u *>(a.adf_v + ab);  // one 16-B load at 8-B alignment
             v[0] = t.x;
             v[1] = t.y;
-            v[2] = nw == 2 ? a.adf_v[ab + 2] : 0.;
+            v[2] = (nw == 2 && !(c_ablate & 8)) ? a.adf_v[ab + 2] : 0.;
         } else {
 #pragma unroll
         for (int c = 0; c <= C; c++) v[c] = (c == 0 || c < nw + 1) ? ld1_s<NT>(a.adf_v + ab + c) : 0.;
@@ -705,10 +705,15 @@ __device__ __forceinline__ void p1_body(MeshPlanDev &mp, const P1Args &a0, int G
             (void)dv;
         } else if (nw > 0) {
             real del_v[C], hn[C], hnn[C], ar[C];
+            if (c_ablate & 16) {
+#pragma unroll
+                for (int c = 0; c < C; c++) del_v[c] = hn[c] = hnn[c] = ar[c] = 1.;
+            } else {
             ldo_s_pre<C, NT, ODD>(a.del_v + b, del_v, last1);
             ldo_s_pre<C, NT, ODD>(a.hnode + b, hn, last1);
             ldo_s_pre<C, NT, ODD>(a.hnode_new + b, hnn, last1);
             ld_nl<C, (OPT & 4) != 0>(a.area + ab, nw, ar, 1.);
+            }
 #pragma unroll
             for (int c = 0; c < C; c++) {
                 const real dta = c < nw ? a.dt / ar[c] : 0.;
