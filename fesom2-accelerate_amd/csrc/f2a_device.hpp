@@ -26,7 +26,8 @@ static constexpr int kBlock = kWave * kWavesPerBlock;
 //   c_ablate        FESOM2_ABLATE, timing-only experiments (results are wrong): bit 0 skips the cluster
 //                   gathers of phase 1, bit 1 its edge gathers, bit 2 the edge gathers of phase 2;
 //                   p1v: bit 3 the second fct_adf_v load (the level below the pair), bit 4 the
-//                   vertical tail's loads (del_ttf_advvert, hnode, hnode_new, area), bit 5 the union DMA
+//                   vertical tail's loads (del_ttf_advvert, hnode, hnode_new, area), bit 5 the union DMA; bit 6
+//                   packed b3h's plus/minus gathers
 //   c_tracer_major  FESOM2_TRACER_MAJOR bits (batched tracers; 1 p1, 2 b3h, 4 p2): tracer-slowest tile
 //                   order; measured: b3h tracer-slowest, p1/p2 tracer-fastest
 //   c_tile_rev      FESOM2_TILE_REV bits (1 p1, 2 b3h, 4 p2): the kernel walks each XCD's tile range

@@ -903,6 +903,11 @@ __global__ __launch_bounds__(1024) void k_b3h_p(const int2 *__restrict__ desc, c
         const bool last1 = ODD && z0[h] + 1 == L;
         ldo_s<C, NT, ODD>(adf_h + (size_t)ei.w * L + z0[h], f[h], last1);
         const size_t i1 = (size_t)ei.x * L + z0[h], i2 = (size_t)ei.y * L + z0[h];
+        if (c_ablate & 64) {  // (timing only: no plus/minus gathers)
+#pragma unroll
+            for (int c = 0; c < C; c++) p1[h][c] = m1[h][c] = p2[h][c] = m2[h][c] = 0.5;
+            continue;
+        }
         ldo<C, ODD>(plus + i1, p1[h], last1);
         ldo<C, ODD>(minus + i1, m1[h], last1);
         ldo<C, ODD>(plus + i2, p2[h], last1);
