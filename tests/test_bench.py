@@ -352,6 +352,12 @@ def test_compact_record_carries_transfers_and_the_emulated_rank():
     out = bench.compact(rec, a, 1)
     assert out["transfers"] == {"h2d_GBps": 30.0}
     assert out["emulated_rank"]["rank"] == 3 and out["emulated_rank"]["of"] == 8
+    assert "single_passes" not in out
+    # a batched leg: the same tracers timed as single-tracer passes ride along
+    sp = {"ms_per_step": 2.2, "batch_gain": round(2.0 / 2.2 - 1, 4)}
+    b = argparse.Namespace(**dict(vars(a), tracers=6, scaling="weak", config="127k x 47", emulate=None))
+    out = bench.compact(dict(rec, single_passes=sp), b, 1)
+    assert out["single_passes"] == sp and out["unit"] == "tracer-cell-updates/s"
 
 
 def test_traffic_is_reported_only_for_the_library_it_measured(tmp_path):
